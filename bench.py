@@ -1,0 +1,320 @@
+#!/usr/bin/env python3
+"""bench.py -- GiB/s of CRC-32 over device-resident batched bodies on 1..8 MI355X.
+
+Metric (BASELINE.json): "GiB/s CRC32 over device-resident batched bodies;
+1/2/4/8 MI355X".  A step = one pass of the batched CRC over the rank's batch
+(one launch of the HIP items kernel).  Default workload = the north star:
+1M x 4 KiB bodies per GPU (weak scaling), synthetic splitmix64 bytes generated
+on the device.  Other BASELINE configs: --config c1 | c2 | c3 | c4.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under
+torch.distributed.run; one process per GPU, RCCL used only as the barrier).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import rpc_amd  # noqa: E402
+from rpc_amd.shard import barrier, max_over_ranks, rank_seed, shard_range, sum_over_ranks  # noqa: E402
+
+METRIC = "GiB/s CRC32 over device-resident batched bodies; 1/2/4/8 MI355X"
+HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+GiB = float(1 << 30)
+
+CONFIGS = {
+    # name: (description, kind, bodies per GPU, body length, seed)
+    "ns": ("north star: 1M x 4 KiB equal-length bodies per GPU", "uniform", 1 << 20, 4096, 0x5EED0003),
+    "c1": ("C1: 1M x 1 KiB equal-length bodies per GPU", "uniform", 1 << 20, 1024, 0x5EED0002),
+    "c2": ("C2: 4M ragged bodies per GPU, log-uniform 64 B-64 KiB, offset/length arrays", "ragged", 1 << 22, 0,
+           0x5EED0004),
+    "c3": ("C3: 8M x 4 KiB bodies per GPU (64M over 8 GPUs)", "uniform", 1 << 23, 4096, 0x5EED0005),
+    "c4": ("C4: 16 x 256 MiB large bodies per GPU, chunked CRC + GF(2) combine", "large", 16, 256 << 20,
+           0x5EED0006),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="ns", choices=sorted(CONFIGS))
+    p.add_argument("--nontemporal", type=int, default=-1, help="-1 = library default")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-inclusive", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
+    return p.parse_args()
+
+
+class Workload:
+    def __init__(self, cfg: str, rank: int, device):
+        desc, kind, n, L, seed = CONFIGS[cfg]
+        self.name, self.desc, self.kind, self.n, self.L = cfg, desc, kind, n, L
+        self.seed = rank_seed(seed, rank)
+        self.device = device
+        if kind == "uniform":
+            self.total = n * L
+            self.base = torch.empty(self.total, dtype=torch.uint8, device=device)
+            self.meta_bytes = 0
+        elif kind == "ragged":
+            from_oracle_free_lengths = _loguniform_lengths(n, self.seed)
+            self.lens_h = from_oracle_free_lengths
+            self.offs_h = np.concatenate([[0], np.cumsum(self.lens_h[:-1], dtype=np.uint64)]).astype(np.uint64)
+            self.total = int(self.lens_h.sum(dtype=np.uint64))
+            self.base = torch.empty(self.total + 8, dtype=torch.uint8, device=device)
+            self.offs = torch.from_numpy(self.offs_h.view(np.int64)).to(device)
+            self.lens = torch.from_numpy(self.lens_h.view(np.int32)).to(device)
+            self.meta_bytes = 12 * n
+        else:  # large
+            self.total = n * L
+            self.base = torch.empty(self.total, dtype=torch.uint8, device=device)
+            self.large_offs = [i * L for i in range(n)]
+            self.large_lens = [L] * n
+            self.meta_bytes = 0
+        rpc_amd.fill_random(self.base, self.seed)
+        self.out = torch.empty(n, dtype=torch.int32, device=device)
+        # algorithmic bytes per launch: body bytes read + metadata read + 4 B/body written
+        self.algo_bytes = self.total + self.meta_bytes + 4 * n
+
+    def step(self):
+        if self.kind == "uniform":
+            rpc_amd.device_uniform(self.base, self.n, self.L, out=self.out)
+        elif self.kind == "ragged":
+            rpc_amd.device_batch(self.base, self.offs, self.lens, out=self.out)
+        else:
+            rpc_amd.device_large(self.base, self.large_offs, self.large_lens, out=self.out)
+
+
+def _loguniform_lengths(n, seed, lo=64, hi=65536):
+    """Same formula as oracle.loguniform_lengths (kept here so the timed GPU leg
+    does not import the oracle)."""
+    k = np.arange(1, n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    ln = np.floor(lo * np.exp(u * np.log(hi / lo))).astype(np.int64)
+    return np.clip(ln, lo, hi).astype(np.uint32)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(w: Workload, target_s: float):
+    """The reference crc.c (+ system libz, built into oracle/_ref) timed on this
+    host's cores over a bounded sample of the same workload."""
+    from oracle import oracle  # cpu_baseline leg only (test/baseline infrastructure)
+    import zlib
+
+    ref = oracle.load_ref()
+    kind = "reference"
+    if ref is None:
+        return None
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    if w.kind == "uniform":
+        nb = min(w.n, (256 << 20) // w.L)
+        host = w.base[: nb * w.L].cpu().numpy()
+        offs = np.arange(nb, dtype=np.uint64) * np.uint64(w.L)
+        lens = np.full(nb, w.L, dtype=np.uint32)
+        sample = f"{nb} x {w.L} B bodies (first {nb * w.L >> 20} MiB of the same device stream)"
+        dev_crc = w.out[:nb].cpu().numpy().view(np.uint32)
+    elif w.kind == "ragged":
+        nb = int(np.searchsorted(np.cumsum(w.lens_h, dtype=np.uint64), 256 << 20))
+        end = int(w.offs_h[nb - 1] + w.lens_h[nb - 1])
+        host = w.base[:end].cpu().numpy()
+        offs, lens = w.offs_h[:nb], w.lens_h[:nb]
+        sample = f"first {nb} ragged bodies ({end >> 20} MiB)"
+        dev_crc = w.out[:nb].cpu().numpy().view(np.uint32)
+    else:
+        host = w.base[: w.L].cpu().numpy()
+        offs = np.array([0], dtype=np.uint64)
+        lens = np.array([w.L], dtype=np.uint32)
+        nb = 1
+        sample = f"1 x {w.L >> 20} MiB body (single-threaded by construction)"
+        dev_crc = w.out[:1].cpu().numpy().view(np.uint32)
+        threads = 1
+    nbytes = int(lens.sum(dtype=np.uint64))
+    s1, crc1 = ref.batch_timed(host, offs, lens, threads=1, reps=1)
+    agree = bool(np.array_equal(crc1, dev_crc))
+    reps = 1
+    sm, _ = ref.batch_timed(host, offs, lens, threads=threads, reps=1)
+    if sm > 0:
+        reps = max(1, min(200, int(math.ceil(target_s / sm))))
+    sm, _ = ref.batch_timed(host, offs, lens, threads=threads, reps=reps)
+    return {
+        "value": round(nbytes * reps / sm / GiB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"{sample}, {reps} passes on {threads} threads ({sm:.1f} s)",
+        "single_thread_value": round(nbytes / s1 / GiB, 3),
+        "cpu_model": cpu_model(),
+        "libz": zlib.ZLIB_RUNTIME_VERSION,
+        "gpu_crcs_match_reference": agree,
+    }
+
+
+def host_inclusive(w: Workload):
+    """Pinned host buffer -> H2D -> kernel -> D2H of CRCs through rpc_crc32_batch."""
+    if w.kind != "uniform":
+        return None
+    nb = min(w.n, (2 << 30) // w.L)
+    host = torch.empty(nb * w.L, dtype=torch.uint8, pin_memory=True)
+    host.copy_(w.base[: nb * w.L])
+    hn = host.numpy()
+    offs = np.arange(nb, dtype=np.uint64) * np.uint64(w.L)
+    lens = np.full(nb, w.L, dtype=np.uint32)
+    best = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        out = rpc_amd.crc32_batch(hn, offs, lens)
+        best = min(best, time.perf_counter() - t0)
+    ok = bool(np.array_equal(out, w.out[:nb].cpu().numpy().view(np.uint32)))
+    return {"GiBps": round(nb * w.L / best / GiB, 2), "bytes": nb * w.L, "matches_device_path": ok}
+
+
+def stream_read_probe(w: Workload, reps=10):
+    """Achievable HBM read rate on the same buffer (coalesced 16-B lanes)."""
+    nbytes = (w.total // 4096) * 4096
+    stream = torch.cuda.current_stream()
+    res = {}
+    for pattern in (0, 1):
+        rpc_amd.stream_read(w.base, pattern, nbytes=nbytes)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            rpc_amd.stream_read(w.base, pattern, nbytes=nbytes)
+        e1.record(stream)
+        e1.synchronize()
+        res[f"pattern{pattern}_GBps"] = round(nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+    return res
+
+
+def load_traffic(cfg: str):
+    """HBM bytes per launch from the committed PMC summary (profiles/), or None."""
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(cfg, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=device)
+    if args.nontemporal >= 0:
+        rpc_amd.set_options(nontemporal=bool(args.nontemporal))
+
+    w = Workload(args.config, rank, device)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        w.step()
+    torch.cuda.synchronize()
+    if dist:
+        barrier(dist, device)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        w.step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        barrier(dist, device)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # avg launch duration on the kernel's stream
+    tmax = max_over_ranks(dist, wall, device) if dist else wall
+    total_bytes = sum_over_ranks(dist, w.total, device) if dist else w.total
+
+    extra = {}
+    cpu = None
+    if rank == 0 and world == 1:
+        extra["stream_read_probe"] = stream_read_probe(w)
+        if not args.no_host_inclusive:
+            extra["host_inclusive"] = host_inclusive(w)
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(w, args.cpu_seconds)
+
+    if rank == 0:
+        achieved = w.algo_bytes / kernel_s / 1e9
+        traffic = load_traffic(args.config)
+        line = {
+            "metric": METRIC,
+            "value": round(total_bytes * args.steps / tmax / GiB, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (counter-based splitmix64 bytes generated on device)",
+            "config": {
+                "workload": w.desc,
+                "bodies_per_gpu": w.n,
+                "body_len": w.L if w.kind != "ragged" else "log-uniform 64..65536",
+                "bytes_per_gpu": w.total,
+                "parallelism": f"dp{world} (payload-index shards, RCCL barrier only)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_BPS / 1e9,
+                "unit": "GB/s",
+                "frac": round(achieved / (HBM_PEAK_BPS / 1e9), 4),
+                "traffic": traffic,
+                "kernel": "crc32_items_kernel" if w.kind != "large" else "crc32_items_kernel (+combine)",
+                "avg_launch_us": round(kernel_s * 1e6, 2),
+                "algo_bytes_per_launch": w.algo_bytes,
+            },
+            "cpu_baseline": cpu,
+            "device": rpc_amd.device_info(),
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

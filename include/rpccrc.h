@@ -1,0 +1,135 @@
+/*
+ * include/rpccrc.h -- C-ABI of librpccrc, the MI355X-native body-checksum
+ * library that replaces KlinLike/RPC's crc.c.
+ *
+ * Drop-in part (exact reference signatures, C linkage, no new types):
+ *   rpc_crc32         replaces reference crc.c:4-9   (declared crc.h:8)
+ *   rpc_crc32_verify  replaces reference crc.c:11-14 (declared crc.h:11)
+ * Callers that keep working unchanged: client/rpc_async.c:219,525 and
+ * server/rpc_server_main.c:227,249 (and the unbuilt client/rpc_client.c:60,154).
+ * Link librpccrc.so in place of crc.c (CMakeLists.txt:14,25).  The library
+ * does NOT define zlib's global `crc32`, so it never interposes on -lz.
+ *
+ * Additive part (SURVEY.md 8b "New (additive) batched ABI"): many-buffer CRC
+ * over host or device (HBM-resident) buffers, computed by hand-written HIP
+ * kernels for gfx950.  Plain pointers and sizes only; the caller owns every
+ * buffer.  `stream` arguments are hipStream_t passed as void* (NULL = the
+ * default stream of the calling thread's current HIP device).
+ *
+ * Semantics are bit-exact to zlib crc32 as called by crc.c:6-7:
+ *   CRC-32/ISO-HDLC, poly 0xEDB88320 (reflected), init/xorout 0xFFFFFFFF;
+ *   rpc_crc32(NULL, n) == 0; rpc_crc32(p, 0) == 0;
+ *   len is reduced modulo 2^32 (zlib's uInt len, crc.c:7 passes size_t).
+ *
+ * Error convention for the int-returning batched calls: 0 (or a non-negative
+ * count where stated) on success, a negative errno-style code on failure
+ * (RPCCRC_E*).  The two drop-in calls have no error channel in the reference
+ * (crc.h:8,11); if no HIP device is usable they print a diagnostic to stderr and
+ * abort() -- they never fall back to a CPU implementation.
+ */
+#pragma once
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define RPCCRC_API __attribute__((visibility("default")))
+#else
+#define RPCCRC_API
+#endif
+
+#define RPCCRC_OK 0
+#define RPCCRC_EINVAL (-22) /* bad argument (NULL buffer with n>0, bad size, ...) */
+#define RPCCRC_ENODEV (-19) /* no usable HIP device */
+#define RPCCRC_ENOMEM (-12) /* device or pinned allocation failed */
+#define RPCCRC_EIO (-5)     /* HIP runtime / kernel launch error */
+
+/* ---- drop-in (reference crc.h) ---------------------------------------- */
+
+/* reference crc.h:8 / crc.c:4-9.  CRC of `len` bytes at `data`. */
+RPCCRC_API uint32_t rpc_crc32(const void *data, size_t len);
+
+/* reference crc.h:11 / crc.c:11-14.  expected_crc in host byte order. */
+RPCCRC_API bool rpc_crc32_verify(const void *data, size_t len, uint32_t expected_crc);
+
+/* ---- batched, host buffers -------------------------------------------- */
+
+/* out_crc[i] = rpc_crc32(base + offsets[i], lengths[i]) for i < n.  Buffers are
+ * host memory (pinned memory is used in place; pageable memory is staged).
+ * flags must be 0.  Returns RPCCRC_OK or a negative code. */
+RPCCRC_API int rpc_crc32_batch(const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, size_t n,
+                    uint32_t *out_crc, int flags);
+
+/* Batched rpc_crc32_verify: ok[i] = (crc == expected[i]).  Returns the number
+ * of mismatching bodies (>= 0) or a negative code. */
+RPCCRC_API int64_t rpc_crc32_verify_batch(const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
+                               const uint32_t *expected, size_t n, uint8_t *ok);
+
+/* ---- batched, device (HBM-resident) buffers ---------------------------- */
+
+/* Ragged batch: body i = d_base[d_offsets[i] .. + d_lengths[i]).  All pointers
+ * are device pointers on the current device.  Asynchronous on `stream`. */
+RPCCRC_API int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                           uint64_t n, uint32_t *d_out, void *stream);
+
+/* Equal-length batch: body i = d_base[i*stride .. + body_len). */
+RPCCRC_API int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_len, uint64_t stride,
+                             uint32_t *d_out, void *stream);
+
+/* Large bodies (any size): body i = d_base[h_offsets[i] .. + h_lengths[i]),
+ * offsets/lengths in HOST memory.  Each body is split into chunk_bytes chunks
+ * (multiple of 16; 0 = default 1 MiB) processed in parallel and merged with
+ * the GF(2) combine (zlib crc32_combine semantics).  Stream-ordered; the call
+ * returns once the work is enqueued. */
+RPCCRC_API int rpc_crc32_device_large(const uint8_t *d_base, const uint64_t *h_offsets, const uint64_t *h_lengths,
+                           uint64_t n, uint32_t *d_out, uint64_t chunk_bytes, void *stream);
+
+/* ---- frames (rpc.h:3-8 wire format) ------------------------------------ */
+
+/* Verify a contiguous device stream of n frames, each a 12-byte big-endian
+ * rpc_header_t {u16 version, u16 type, u32 body_len, u32 crc32} followed by
+ * body_len body bytes (reference rpc.h:3-15; parse as rpc_server_main.c:165-169).
+ * d_frame_offsets[i] = byte offset of frame i's header.  d_ok[i] = 1 when the
+ * body CRC equals the header CRC (PING/PONG frames with body_len 0 and crc 0
+ * verify as 1, as rpc_server_main.c:172-187 short-circuits them). */
+RPCCRC_API int rpc_frames_verify_device(const uint8_t *d_stream, const uint64_t *d_frame_offsets, uint64_t n,
+                             uint8_t *d_ok, uint32_t *d_crc, void *stream);
+
+/* Stamp headers: for each frame i write its 12-byte header (version, type,
+ * body_len, crc32 big-endian, as rpc_async.c:521-530) at d_stream +
+ * d_frame_offsets[i]; the body must already follow the header. */
+RPCCRC_API int rpc_frames_stamp_device(uint8_t *d_stream, const uint64_t *d_frame_offsets, const uint32_t *d_body_lens,
+                            uint64_t n, uint16_t version, uint16_t type, void *stream);
+
+/* ---- helpers ----------------------------------------------------------- */
+
+/* zlib crc32_combine (zlib.h:1750): crc(A||B) from crc(A), crc(B), |B|. */
+RPCCRC_API uint32_t rpc_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+
+/* Fill d_dst with the counter-based splitmix64 stream used by tests/bench
+ * (word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15), little-endian).
+ * nbytes must be a multiple of 8. */
+RPCCRC_API int rpc_crc32_fill_random_device(void *d_dst, uint64_t nbytes, uint64_t seed, void *stream);
+
+/* HBM read probe over nbytes (multiple of 4096): pattern 0 = coalesced 16-B
+ * lanes, 1 = the CRC kernel's 64-B-per-lane segments. */
+RPCCRC_API int rpc_crc32_stream_read_device(const void *d_src, uint64_t nbytes, int pattern, int nontemporal, void *stream);
+
+/* Tuning knobs (process-wide): nontemporal loads (0/1, default 0) and the
+ * persistent-grid size cap in workgroups (0 = one per CU). */
+RPCCRC_API int rpc_crc32_set_options(int nontemporal, int max_blocks);
+
+/* Human-readable text for a negative return code. */
+RPCCRC_API const char *rpc_crc32_strerror(int err);
+
+/* Writes "device=<name> arch=<gcn> cus=<n>" for the current device. */
+RPCCRC_API int rpc_crc32_device_info(char *buf, size_t buflen);
+
+#ifdef __cplusplus
+}
+#endif

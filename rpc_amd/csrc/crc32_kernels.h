@@ -1,0 +1,43 @@
+// rpc_amd/csrc/crc32_kernels.h -- internal (C++) interface between the C-ABI
+// host layer (rpccrc_api.cpp) and the HIP kernels (crc32_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rpccrc {
+
+// Output modes of the items kernel.
+constexpr uint32_t kModeFinal = 0; // crc(M) = ~U(F, M)           (rpc_crc32 value)
+constexpr uint32_t kModeRaw = 1;   // crc0(M)                      (chunk partials)
+constexpr uint32_t kModeInit = 2;  // U(F, M), no final complement (diagnostic)
+
+struct ItemsArgs {
+  const uint8_t *base;      // device (or host-mapped) byte buffer
+  const uint64_t *offsets;  // nullptr -> item i at i * stride
+  const uint32_t *lengths;  // nullptr -> every item has length len
+  uint64_t n_items;
+  uint64_t stride;
+  uint32_t len;
+  uint32_t mode;
+  const uint4 *lds_image;   // kLdsBytes of table image for the chosen G
+  const uint32_t *tq;       // Tq[q] = A_q(0xFFFFFFFF), q = 0..4096
+  uint32_t *out;            // n_items CRCs
+};
+
+struct CombineArgs {
+  const uint32_t *raw;          // per-chunk crc0 values
+  const uint64_t *lengths;      // body lengths (bytes)
+  const uint64_t *chunk_first;  // index into raw of each body's chunk 0
+  const uint32_t *x2n_bytes;    // x^(8*2^k) mod P, k = 0..63
+  uint64_t n_bodies;
+  uint64_t chunk;               // chunk size in bytes (multiple of 16)
+  uint32_t *out;
+};
+
+hipError_t launch_items(const ItemsArgs &a, int G, bool nt, int max_blocks, hipStream_t stream);
+hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream);
+hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream);
+hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool nt, int max_blocks, uint32_t *out,
+                              hipStream_t stream);
+
+} // namespace rpccrc

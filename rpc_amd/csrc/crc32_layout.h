@@ -1,0 +1,43 @@
+// rpc_amd/csrc/crc32_layout.h -- LDS table image layout of the batched kernel.
+//
+// One persistent 1024-thread workgroup per CU owns 156 KiB of LDS holding every
+// table the kernel looks up.  All lookups are ds_read_b32 whose bank is
+// (byte_addr/4) mod 32 (MI355X_MICROARCH.md, LDS table): a table replicated 32
+// times with copy c = lane & 31 at bank c is conflict-free for ANY indices.
+//
+//   MAIN   [0, 128 KiB)  slice-by-4 byte tables, 32 copies, two tables per
+//                        256-byte row so that one v_perm_b32 forms the address:
+//                        region 0: row v = { T3[v] x32 | T2[v] x32 }
+//                        region 1: row v = { T1[v] x32 | T0[v] x32 } (+64 KiB)
+//   S1     16 KiB        per-lane shift, step 1 (nibble tables, 32 copies):
+//                        S1[n][nib][c] = A_{64*(7-(c&7))}(nib << 4n)
+//   S2     4 KiB         per-lane shift, step 2 (nibble tables, 8 groups):
+//                        S2[n][nib][h] = A_{512*(G/8-1-(h & (G/8-1)))}(nib << 4n)
+//   RW     512 B         row Horner step: RW[n][nib] = A_{ROW}(nib << 4n)
+//   ZI     7.5 KiB       trailing-pad undo: ZI[z-1][n][nib] = A_z^-1(nib << 4n)
+//
+// ROW = 64 lanes-per-group(G) * 64 bytes-per-lane-segment; G in {16, 64}.
+#pragma once
+#include <stdint.h>
+
+namespace rpccrc {
+
+constexpr uint32_t kSegBytes = 64;           // bytes per lane per row
+constexpr uint32_t kLdsMain = 0;
+constexpr uint32_t kLdsMainRegion1 = 65536;
+constexpr uint32_t kLdsS1 = 131072;
+constexpr uint32_t kLdsS2 = kLdsS1 + 16384;  // 147456
+constexpr uint32_t kLdsRW = kLdsS2 + 4096;   // 151552
+constexpr uint32_t kLdsZI = kLdsRW + 512;    // 152064
+constexpr uint32_t kLdsBytes = kLdsZI + 15 * 512; // 159744 (156 KiB)
+constexpr uint32_t kLdsWords = kLdsBytes / 4;
+constexpr uint32_t kMaxRow = 64 * kSegBytes; // 4096
+constexpr uint32_t kTqEntries = kMaxRow + 1; // Tq[q] = A_q(0xFFFFFFFF), q=0..4096
+
+constexpr uint32_t row_bytes(int G) { return (uint32_t)G * kSegBytes; }
+
+// Host-side builders (crc32_tables.cpp).
+void build_lds_image(int G, uint32_t *img /* kLdsWords */);
+void build_tq(uint32_t *tq /* kTqEntries */);
+
+} // namespace rpccrc

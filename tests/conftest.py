@@ -1,0 +1,25 @@
+"""Shared pytest setup.  `gpu` marks tests that need a real MI355X (run with -m gpu)."""
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(REPO, "tests", "golden", "crc32_golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def repo_root():
+    return REPO

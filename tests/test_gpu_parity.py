@@ -1,0 +1,339 @@
+"""GPU parity: the HIP path (through librpccrc's C-ABI) against the CPU oracle and the
+reference golden vectors.  Bit-exact everywhere (integer/byte work).
+
+Small sizes are compared body by body against the oracle; BASELINE.json's full
+sizes are checked with size-independent properties (sampled oracle parity,
+linearity crc(X)^crc(Y)^crc(X^Y) == crc(0^L), and a checksum of checksums:
+the whole buffer as ONE body through the chunked path equals the zlib
+crc32_combine fold of the per-body CRCs).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import rpc_amd  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def to_dev(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    torch.cuda.set_device(0)
+    info = rpc_amd.device_info()
+    assert "gfx950" in info, info
+    yield
+
+
+# ---- drop-in rpc_crc32 / rpc_crc32_verify (crc.c:4-14) ----------------------
+
+def test_drop_in_kats(golden):
+    for k in golden["kats"]:
+        b = bytes.fromhex(k["hex"])
+        assert rpc_amd.rpc_crc32(b) == k["crc"], k["name"]
+        assert rpc_amd.rpc_crc32_verify(b, k["crc"])
+        assert not rpc_amd.rpc_crc32_verify(b, k["crc"] ^ 1)
+
+
+def test_drop_in_edges(golden):
+    assert rpc_amd.rpc_crc32(None, 5) == 0
+    assert rpc_amd.rpc_crc32(b"abc", 0) == 0
+    # zlib uInt length: 2**32 + 3 reads exactly 3 bytes
+    assert rpc_amd.rpc_crc32(bytes(3), 2**32 + 3) == golden["edges"]["zeros3"]
+
+
+def test_drop_in_golden_random(golden):
+    for r in golden["random_bodies"]:
+        data = oracle.splitmix_bytes(r["len"], r["seed"])
+        assert rpc_amd.rpc_crc32(data) == r["crc"], r
+
+
+def test_drop_in_large_bodies():
+    for n in [(8 << 20) - 1, (8 << 20) + 13, (17 << 20) + 5]:  # device copy and chunked paths
+        data = oracle.splitmix_bytes(n, n)
+        assert rpc_amd.rpc_crc32(data) == oracle.crc32(data), n
+
+
+def test_drop_in_frames(golden):
+    """The captured wire frames: header CRC == rpc_crc32(body)."""
+    for f in golden["frames"]:
+        hdr = bytes.fromhex(f["header_hex"])
+        body = f["body"].encode()
+        assert rpc_amd.rpc_crc32_verify(body, int.from_bytes(hdr[8:12], "big"))
+
+
+def test_drop_in_thread_safety():
+    rng = np.random.default_rng(3)
+    bodies = [rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes() for _ in range(400)]
+    want = [oracle.crc32(b) for b in bodies]
+    errors = []
+
+    def worker(k):
+        for i in range(k, len(bodies), 8):
+            if rpc_amd.rpc_crc32(bodies[i]) != want[i]:
+                errors.append(i)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+
+
+# ---- device batches ------------------------------------------------------------
+
+@pytest.mark.parametrize("body_len", [1, 3, 4, 15, 16, 17, 63, 64, 100, 1000, 1023, 1024, 1025, 2000, 4080,
+                                      4095, 4096, 4097, 4100, 8192, 12345, 65536])
+@pytest.mark.parametrize("pad", [0, 7])
+def test_device_uniform(body_len, pad):
+    stride = body_len + pad
+    n = max(1, min(3000, (6 << 20) // stride))
+    host = oracle.splitmix_bytes(n * stride + 16, body_len * 31 + pad)
+    base = to_dev(host)
+    got = u32(rpc_amd.device_uniform(base, n, body_len, stride))
+    assert np.array_equal(got, oracle.crc32_uniform(host, n, body_len, stride))
+
+
+@pytest.mark.parametrize("misalign", [0, 1, 3, 8, 13])
+def test_device_batch_ragged(misalign):
+    rng = np.random.default_rng(100 + misalign)
+    lens = rng.integers(0, 70000, 600).astype(np.uint32)
+    lens[::37] = 0
+    lens[5] = 1
+    lens[6] = 65536
+    offs = (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]) + misalign).astype(np.uint64)
+    host = oracle.splitmix_bytes(int(lens.sum()) + misalign + 16, 77 + misalign)
+    got = u32(rpc_amd.device_batch(to_dev(host), to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    assert np.array_equal(got, oracle.crc32_batch(host, offs, lens))
+
+
+def test_device_batch_unordered_overlapping():
+    """Offsets in any order, bodies may overlap (each is an independent view)."""
+    rng = np.random.default_rng(9)
+    host = oracle.splitmix_bytes(1 << 20, 5)
+    lens = rng.integers(0, 20000, 500).astype(np.uint32)
+    offs = rng.integers(0, (1 << 20) - 20000, 500).astype(np.uint64)
+    got = u32(rpc_amd.device_batch(to_dev(host), to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    assert np.array_equal(got, oracle.crc32_batch(host, offs, lens))
+
+
+def test_device_golden_random_bodies(golden):
+    rb = golden["random_bodies"]
+    parts = [oracle.splitmix_bytes(r["len"], r["seed"]) for r in rb]
+    lens = np.array([r["len"] for r in rb], dtype=np.uint32)
+    offs = (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]) + 3).astype(np.uint64)
+    host = np.concatenate([np.zeros(3, np.uint8)] + parts + [np.zeros(16, np.uint8)])
+    got = u32(rpc_amd.device_batch(to_dev(host), to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    assert got.tolist() == [r["crc"] for r in rb]
+
+
+def test_device_json_c0(golden):
+    """Config C0: 1024 x 4 KiB JSON-RPC bodies (the reference's CPU case) on the device."""
+    buf, offs, lens = oracle.json_bodies(1024, 4096, 0x5EED0001)
+    got = u32(rpc_amd.device_uniform(to_dev(buf), 1024, 4096))
+    assert np.array_equal(got, oracle.crc32_batch(buf, offs, lens))
+    assert got[:16].tolist() == golden["json_c0"]["crcs"]
+
+
+@pytest.mark.parametrize("chunk", [0, 65536, 4096 + 16])
+def test_device_large(chunk):
+    lens = [0, 1, 17, 4096, (5 << 20) + 3, (33 << 20) + 11]
+    offs, pos = [], 5
+    for L in lens:
+        offs.append(pos)
+        pos += L + 3
+    host = oracle.splitmix_bytes(pos + 16, 1234)
+    got = u32(rpc_amd.device_large(to_dev(host), offs, lens, chunk=chunk))
+    want = [oracle.crc32(host[o:o + L]) for o, L in zip(offs, lens)]
+    assert got.tolist() == want
+
+
+def test_nontemporal_option_same_result():
+    host = oracle.splitmix_bytes(4096 * 500, 8)
+    base = to_dev(host)
+    a = u32(rpc_amd.device_uniform(base, 500, 4096))
+    rpc_amd.set_options(nontemporal=True)
+    try:
+        b = u32(rpc_amd.device_uniform(base, 500, 4096))
+    finally:
+        rpc_amd.set_options(nontemporal=False)
+    assert np.array_equal(a, b)
+
+
+def test_fill_random_matches_oracle_stream():
+    t = torch.empty(1 << 20, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(t, 0x5EED0003)
+    assert np.array_equal(t.cpu().numpy(), oracle.splitmix_bytes(1 << 20, 0x5EED0003))
+
+
+# ---- host-buffer batch API --------------------------------------------------------
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_batch(pinned):
+    rng = np.random.default_rng(21)
+    lens = rng.integers(0, 40000, 3000).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64) + 1
+    host = oracle.splitmix_bytes(int(lens.sum()) + 32, 4)
+    if pinned:
+        pt = torch.from_numpy(host).pin_memory()
+        host = pt.numpy()
+    got = rpc_amd.crc32_batch(host, offs, lens)
+    assert np.array_equal(got, oracle.crc32_batch(host, offs, lens))
+    exp = got.copy()
+    exp[::5] ^= 1
+    bad, ok = rpc_amd.verify_batch(host, offs, lens, exp)
+    assert bad == len(exp[::5]) and ok[1] == 1 and ok[0] == 0
+
+
+def test_host_batch_spans_many_stages():
+    """> 256 MiB stage: exercises the double-buffered H2D pipeline and the large-body path."""
+    n, L = 80, 4 << 20
+    host = np.empty(n * L + (300 << 20), dtype=np.uint8)
+    host[: n * L] = np.tile(oracle.splitmix_bytes(L, 6), n)
+    host[n * L:] = oracle.splitmix_bytes(300 << 20, 7)
+    offs = np.array([i * L for i in range(n)] + [n * L], dtype=np.uint64)
+    lens = np.array([L] * n + [300 << 20], dtype=np.uint32)
+    got = rpc_amd.crc32_batch(host, offs, lens)
+    c = oracle.crc32(host[:L])
+    assert (got[:n] == c).all()
+    assert got[n] == oracle.crc32(host[n * L:])
+
+
+# ---- frames (rpc.h wire format) ----------------------------------------------------
+
+def _build_frames(bodies, gap=0):
+    offs, blob = [], bytearray()
+    for b in bodies:
+        offs.append(len(blob))
+        blob += bytes(12) + b + bytes(gap)
+    return bytearray(blob), np.array(offs, dtype=np.uint64)
+
+
+def test_frames_verify_and_stamp(golden):
+    rng = np.random.default_rng(2)
+    bodies = [f["body"].encode() for f in golden["frames"]]
+    bodies += [rng.integers(32, 127, int(rng.integers(0, 1025)), dtype=np.uint8).tobytes() for _ in range(300)]
+    blob, offs = _build_frames(bodies, gap=1)
+    lens = np.array([len(b) for b in bodies], dtype=np.uint32)
+    dblob = to_dev(np.frombuffer(bytes(blob), dtype=np.uint8).copy())
+    rpc_amd.frames_stamp(dblob, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32)), version=1,
+                         type_=rpc_amd.RPC_TYPE_DATA)
+    stamped = dblob.cpu().numpy().tobytes()
+    for i, (o, b) in enumerate(zip(offs, bodies)):
+        hdr = stamped[int(o):int(o) + 12]
+        want = (1).to_bytes(2, "big") + (0).to_bytes(2, "big") + len(b).to_bytes(4, "big") + \
+            oracle.crc32(b).to_bytes(4, "big")
+        assert hdr == want, i
+    # the captured request/response headers are reproduced byte for byte
+    assert stamped[:12].hex() == golden["frames"][0]["header_hex"]
+    assert stamped[int(offs[1]):int(offs[1]) + 12].hex() == golden["frames"][1]["header_hex"]
+    # corrupt some bodies / CRC fields, then verify
+    arr = np.frombuffer(stamped, dtype=np.uint8).copy()
+    bad = set()
+    for i in range(4, len(bodies), 7):
+        if lens[i] > 0:
+            arr[int(offs[i]) + 12 + int(lens[i]) // 2] ^= 0x10
+        else:
+            arr[int(offs[i]) + 11] ^= 1
+        bad.add(i)
+    ok, crc = rpc_amd.frames_verify(to_dev(arr), to_dev(offs.view(np.int64)))
+    ok = ok.cpu().numpy()
+    for i in range(len(bodies)):
+        assert ok[i] == (0 if i in bad else 1), i
+    body_crc = [oracle.crc32(arr[int(o) + 12:int(o) + 12 + int(L)]) for o, L in zip(offs, lens)]
+    assert u32(crc).tolist() == body_crc
+
+
+def test_frames_ping_pong(golden):
+    hdrs = b"".join(bytes.fromhex(f["header_hex"]) for f in golden["frames"][2:])
+    ok, _ = rpc_amd.frames_verify(to_dev(np.frombuffer(hdrs, np.uint8).copy()),
+                                  to_dev(np.array([0, 12], dtype=np.int64)))
+    assert ok.cpu().tolist() == [1, 1]
+
+
+# ---- BASELINE.json full sizes: size-independent properties --------------------------
+
+def _sample_check(base_dev, n, L, stride, got, k=1500, seed=0):
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(n, size=min(k, n), replace=False)
+    for i in idx:
+        body = base_dev[int(i) * stride:int(i) * stride + L].cpu().numpy()
+        assert got[i] == oracle.crc32(body), int(i)
+
+
+def _linearity(n, L, seed_x, seed_y):
+    x = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    y = torch.empty_like(x)
+    rpc_amd.fill_random(x, seed_x)
+    rpc_amd.fill_random(y, seed_y)
+    cx = u32(rpc_amd.device_uniform(x, n, L))
+    cy = u32(rpc_amd.device_uniform(y, n, L))
+    xy = torch.bitwise_xor(x, y)
+    cxy = u32(rpc_amd.device_uniform(xy, n, L))
+    zero = oracle.crc32(bytes(L))
+    assert np.all((cx ^ cy ^ cxy) == zero)
+    return x, cx
+
+
+def test_north_star_1M_x_4KiB():
+    n, L = 1 << 20, 4096
+    x, cx = _linearity(n, L, 0x5EED0003, 0x5EED0013)
+    _sample_check(x, n, L, L, cx)
+    # checksum of checksums: the whole 4 GiB as one body == fold of per-body CRCs
+    whole = u32(rpc_amd.device_large(x, [0], [n * L]))[0]
+    acc = int(cx[0])
+    for c in cx[1:]:
+        acc = oracle.combine(acc, int(c), L)
+    assert whole == acc
+
+
+def test_c1_1M_x_1KiB():
+    n, L = 1 << 20, 1024
+    x, cx = _linearity(n, L, 0x5EED0002, 0x5EED0012)
+    _sample_check(x, n, L, L, cx, seed=1)
+
+
+def test_c2_ragged_loguniform_sample():
+    n = 1 << 19  # 1/8 of config C2's 4M bodies (same distribution), ~4.6 GiB
+    lens = oracle.loguniform_lengths(n, 0x5EED0004)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum())
+    base = torch.empty(total + 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0x5EED0004)
+    got = u32(rpc_amd.device_batch(base, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    rng = np.random.default_rng(4)
+    for i in rng.choice(n, 1500, replace=False):
+        body = base[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy()
+        assert got[i] == oracle.crc32(body), int(i)
+
+
+def test_c4_large_bodies():
+    n, L = 16, 256 << 20
+    base = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0x5EED0006)
+    got = u32(rpc_amd.device_large(base, [i * L for i in range(n)], [L] * n))
+    # body 0 and 15 fully against the oracle (256 MiB each on the CPU)
+    for i in (0, n - 1):
+        assert got[i] == oracle.crc32(base[i * L:(i + 1) * L].cpu().numpy())
+    # every body: per-1MiB-chunk uniform CRCs folded with crc32_combine
+    sub = 1 << 20
+    per = u32(rpc_amd.device_uniform(base, n * (L // sub), sub))
+    for i in range(n):
+        acc = int(per[i * (L // sub)])
+        for c in per[i * (L // sub) + 1:(i + 1) * (L // sub)]:
+            acc = oracle.combine(acc, int(c), sub)
+        assert got[i] == acc
