@@ -19,7 +19,7 @@ struct ItemsArgs {
   uint64_t stride;
   uint32_t len;
   uint32_t mode;
-  const uint4 *lds_image;   // kLdsBytes of table image for the chosen G
+  const uint4 *lds_image;   // LDS table image (v2 layout, kLdsBytesV2 bytes)
   const uint32_t *tq;       // Tq[q] = A_q(0xFFFFFFFF), q = 0..4096
   uint32_t *out;            // n_items CRCs
 };
@@ -34,7 +34,9 @@ struct CombineArgs {
   uint32_t *out;
 };
 
-hipError_t launch_items(const ItemsArgs &a, int G, bool nt, int max_blocks, hipStream_t stream);
+// QB = 1: rows of 4 KiB of one item (any length); QB = 4: four items per row,
+// each with len + ((-(end address)) & 15) <= 1024.
+hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream);
 hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream);
 hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream);
 hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool nt, int max_blocks, uint32_t *out,

@@ -68,6 +68,41 @@ void build_lds_image(int G, uint32_t *img) {
   }
 }
 
+void build_lds_image_v2(uint32_t *img) {
+  memset(img, 0, kLdsBytesV2);
+  uint8_t *b = reinterpret_cast<uint8_t *>(img);
+  auto put = [&](uint32_t byte_addr, uint32_t v) { memcpy(b + byte_addr, &v, 4); };
+  for (uint32_t v = 0; v < 256; ++v) {
+    const uint32_t t0 = crc_slice_entry(0, v), t1 = crc_slice_entry(1, v);
+    const uint32_t t2 = crc_slice_entry(2, v), t3 = crc_slice_entry(3, v);
+    for (uint32_t c = 0; c < 32; ++c) {
+      put(kLdsMain + v * 256 + c * 4, t3);
+      put(kLdsMain + v * 256 + 128 + c * 4, t2);
+      put(kLdsMainRegion1 + v * 256 + c * 4, t1);
+      put(kLdsMainRegion1 + v * 256 + 128 + c * 4, t0);
+    }
+  }
+  uint32_t nt[8][16];
+  for (uint32_t c = 0; c < 32; ++c) { // hi = c & 3
+    nibble_table(1024u * (3u - (c & 3u)), nt);
+    for (int n = 0; n < 8; ++n)
+      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsSH + n * 2048 + nib * 128 + c * 4, nt[n][nib]);
+  }
+  for (uint32_t lo = 0; lo < 16; ++lo) {
+    nibble_table(64u * (15u - lo), nt);
+    for (int n = 0; n < 8; ++n)
+      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsSL + n * 1024 + nib * 64 + lo * 4, nt[n][nib]);
+  }
+  nibble_table(4096u, nt);
+  for (int n = 0; n < 8; ++n)
+    for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsRW2 + n * 64 + nib * 4, nt[n][nib]);
+  for (uint32_t z = 1; z <= 15; ++z) {
+    nibble_table_inverse(z, nt);
+    for (int n = 0; n < 8; ++n)
+      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsZI2 + (z - 1) * 512 + n * 64 + nib * 4, nt[n][nib]);
+  }
+}
+
 void build_tq(uint32_t *tq) {
   for (uint32_t q = 0; q < kTqEntries; ++q) tq[q] = gf2_shift_bytes(0xFFFFFFFFu, q);
 }

@@ -31,8 +31,7 @@ constexpr int kMaxDevices = 64;
 struct DeviceCtx {
   int device = -1;
   int cus = 0;
-  uint4 *img16 = nullptr; // LDS image, G = 16
-  uint4 *img64 = nullptr; // LDS image, G = 64
+  uint4 *img = nullptr;   // LDS table image (v2 layout, 160 KiB)
   uint32_t *tq = nullptr;
   uint32_t *x2n = nullptr; // x^(8*2^k) mod P, k = 0..63
   int status = RPCCRC_ENODEV;
@@ -71,13 +70,13 @@ void init_device(int dev) {
   c.cus = prop.multiProcessorCount;
   snprintf(c.name, sizeof c.name, "%s", prop.name);
   snprintf(c.arch, sizeof c.arch, "%s", prop.gcnArchName);
-  if (prop.sharedMemPerBlock < kLdsBytes) { // needs the 160 KiB LDS of gfx950
+  if (prop.sharedMemPerBlock < kLdsBytesV2) { // needs the 160 KiB LDS of gfx950
     fprintf(stderr, "rpccrc: device %d (%s) has %zu B LDS per block, need %u\n", dev, c.arch,
-            (size_t)prop.sharedMemPerBlock, kLdsBytes);
+            (size_t)prop.sharedMemPerBlock, kLdsBytesV2);
     c.status = RPCCRC_ENODEV;
     return;
   }
-  std::vector<uint32_t> img(kLdsWords), tq(kTqEntries), x2n(64);
+  std::vector<uint32_t> img(kLdsBytesV2 / 4), tq(kTqEntries), x2n(64);
   build_tq(tq.data());
   uint32_t sq = kX0 >> 8; // x^8 (one zero byte)
   for (int k = 0; k < 64; ++k) {
@@ -88,17 +87,12 @@ void init_device(int dev) {
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);
   hipError_t e = hipSuccess;
-  e = (e == hipSuccess) ? hipMalloc(&c.img16, kLdsBytes) : e;
-  e = (e == hipSuccess) ? hipMalloc(&c.img64, kLdsBytes) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.img, kLdsBytesV2) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.x2n, 64 * 4) : e;
   if (e == hipSuccess) {
-    build_lds_image(16, img.data());
-    e = hipMemcpy(c.img16, img.data(), kLdsBytes, hipMemcpyHostToDevice);
-  }
-  if (e == hipSuccess) {
-    build_lds_image(64, img.data());
-    e = hipMemcpy(c.img64, img.data(), kLdsBytes, hipMemcpyHostToDevice);
+    build_lds_image_v2(img.data());
+    e = hipMemcpy(c.img, img.data(), kLdsBytesV2, hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.x2n, x2n.data(), 64 * 4, hipMemcpyHostToDevice);
@@ -125,7 +119,7 @@ int max_blocks_for(const DeviceCtx &c) {
 }
 
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int G, hipStream_t s) {
+          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
   ItemsArgs a;
   a.base = base;
   a.offsets = offsets;
@@ -134,10 +128,10 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   a.stride = stride;
   a.len = len;
   a.mode = mode;
-  a.lds_image = (G == 16) ? c.img16 : c.img64;
+  a.lds_image = c.img;
   a.tq = c.tq;
   a.out = out;
-  return map_hip(launch_items(a, G, g_nontemporal != 0, max_blocks_for(c), s));
+  return map_hip(launch_rows(a, QB, g_nontemporal != 0, max_blocks_for(c), s));
 }
 
 // ---- large bodies: chunk expansion + combine --------------------------------
@@ -236,7 +230,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
                      chunk, total, d_ioff, d_ilen, d_lens, d_firsts);
   e = hipGetLastError();
   int r = map_hip(e);
-  if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 64, s);
+  if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
   if (r == RPCCRC_OK) {
     CombineArgs ca;
     ca.raw = d_raw;
@@ -300,7 +294,7 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
         die("pinned alloc", RPCCRC_ENOMEM);
     }
     memcpy(t.pin, src, len);
-    rc = items(*c, t.pin, nullptr, nullptr, 1, 0, len, kModeFinal, t.pout, len <= 1024 ? 16 : 64, t.stream);
+    rc = items(*c, t.pin, nullptr, nullptr, 1, 0, len, kModeFinal, t.pout, 1, t.stream);
   } else {
     if (t.dcap < len) {
       if (t.dbuf) (void)hipFree(t.dbuf);
@@ -313,7 +307,7 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
       const uint64_t off = 0, l64 = len;
       rc = device_large(*c, t.dbuf, &off, &l64, 1, t.pout, 0, t.stream);
     } else {
-      rc = items(*c, t.dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, t.pout, 64, t.stream);
+      rc = items(*c, t.dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, t.pout, 1, t.stream);
     }
   }
   if (rc) die("kernel launch", rc);
@@ -425,7 +419,7 @@ int host_batch(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets,
     if (hi > lo) RPCCRC_TRY(hipMemcpyAsync(s.dbuf, base + lo, hi - lo, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.doff, s.hoff, cnt * 8, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.dlen, s.hlen, cnt * 4, hipMemcpyHostToDevice, s.stream));
-    rc = items(c, s.dbuf, s.doff, s.dlen, cnt, 0, 0, kModeFinal, s.dout, 64, s.stream);
+    rc = items(c, s.dbuf, s.doff, s.dlen, cnt, 0, 0, kModeFinal, s.dout, 1, s.stream);
     if (rc) return rc;
     RPCCRC_TRY(hipMemcpyAsync(s.hout, s.dout, cnt * 4, hipMemcpyDeviceToHost, s.stream));
     s.first = i;
@@ -503,8 +497,11 @@ int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_le
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) return rc;
-  const int G = body_len <= 1024 ? 16 : 64;
-  return items(*c, d_base, nullptr, nullptr, n, stride, body_len, kModeFinal, d_out, G,
+  // Four bodies per 4 KiB row when every body plus its pad to a 16-byte end
+  // fits a 1 KiB quarter (QB = 4); otherwise one body per row sequence.
+  const uint32_t zmax = (stride % 16 == 0) ? (uint32_t)(0u - (uint32_t)(uintptr_t)(d_base + body_len)) & 15u : 15u;
+  const int QB = (body_len + zmax <= 1024) ? 4 : 1;
+  return items(*c, d_base, nullptr, nullptr, n, stride, body_len, kModeFinal, d_out, QB,
                static_cast<hipStream_t>(stream));
 }
 
@@ -534,7 +531,7 @@ int rpc_frames_verify_device(const uint8_t *d_stream, const uint64_t *d_frame_of
   uint32_t *bexp = blen + n;
   uint32_t *bcrc = d_crc ? d_crc : bexp + n;
   rc = map_hip(launch_frames_parse(d_stream, d_frame_offsets, n, boff, blen, bexp, s));
-  if (rc == RPCCRC_OK) rc = items(*c, d_stream, boff, blen, n, 0, 0, kModeFinal, bcrc, 64, s);
+  if (rc == RPCCRC_OK) rc = items(*c, d_stream, boff, blen, n, 0, 0, kModeFinal, bcrc, 1, s);
   if (rc == RPCCRC_OK) rc = map_hip(launch_frames_compare(bcrc, bexp, n, d_ok, s));
   (void)hipFreeAsync(ws, s);
   return rc;
@@ -553,7 +550,7 @@ int rpc_frames_stamp_device(uint8_t *d_stream, const uint64_t *d_frame_offsets, 
   uint64_t *boff = reinterpret_cast<uint64_t *>(ws);
   uint32_t *bcrc = reinterpret_cast<uint32_t *>(boff + n);
   rc = map_hip(launch_frames_body_offsets(d_frame_offsets, n, boff, s));
-  if (rc == RPCCRC_OK) rc = items(*c, d_stream, boff, d_body_lens, n, 0, 0, kModeFinal, bcrc, 64, s);
+  if (rc == RPCCRC_OK) rc = items(*c, d_stream, boff, d_body_lens, n, 0, 0, kModeFinal, bcrc, 1, s);
   if (rc == RPCCRC_OK)
     rc = map_hip(launch_frames_stamp(d_stream, d_frame_offsets, d_body_lens, bcrc, n, version, type, s));
   (void)hipFreeAsync(ws, s);

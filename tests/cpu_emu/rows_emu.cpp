@@ -1,0 +1,233 @@
+// tests/cpu_emu/rows_emu.cpp -- CPU emulation of crc32_rows_kernel (v2) lane by
+// lane (TEST CODE): coalesced piece loads, the DPP lane-pair transpose, the
+// slice-by-4 chain on the v2 LDS image, SH/SL nibble steps with the exact DPP /
+// swizzle reduction patterns, Horner, Tq, ZI.  Compared with the oracle by
+// tests/test_kernel_emu.py.  Not the product path.
+//
+// stdin:  QB misalign n  then n lengths; bodies are splitmix bytes (seed 7)
+//         back to back from byte `misalign` of a 16-aligned buffer.
+// stdout: one CRC (hex) per body.
+#include "../../rpc_amd/csrc/crc32_gf2.h"
+#include "../../rpc_amd/csrc/crc32_layout.h"
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+using namespace rpccrc;
+
+static std::vector<uint32_t> g_img, g_tq;
+static uint32_t ld(uint32_t a) {
+  if (a % 4 || a >= kLdsBytesV2) { fprintf(stderr, "bad lds addr %u\n", a); exit(2); }
+  return g_img[a / 4];
+}
+static uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  uint64_t data = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int b = 0; b < 4; ++b) {
+    uint32_t sb = (sel >> (8 * b)) & 0xFF;
+    uint32_t out = sb >= 13 ? 0xFF : sb == 12 ? 0 : sb <= 7 ? (uint32_t)(data >> (8 * sb)) & 0xFF : 0;
+    r |= out << (8 * b);
+  }
+  return r;
+}
+static uint32_t slice4(uint32_t x, uint32_t lsel) {
+  return ld(perm(x, lsel, 0x0C0C0400u)) ^ ld(perm(x, lsel, 0x0C0C0501u)) ^ ld(perm(x, lsel, 0x0C020600u)) ^
+         ld(perm(x, lsel, 0x0C020701u));
+}
+static uint32_t nib_map(uint32_t s, uint32_t base, uint32_t stride, uint32_t shift) {
+  uint32_t r = 0;
+  for (uint32_t n = 0; n < 8; ++n) r ^= ld(base + n * stride + (((s >> (4 * n)) & 15u) << shift));
+  return r;
+}
+typedef uint32_t Wave[64];
+static void quad_perm(const Wave in, Wave out, const int p[4]) {
+  for (int l = 0; l < 64; ++l) out[l] = in[(l & ~3) | p[l & 3]];
+}
+static void row_ror(const Wave in, Wave out, int n) { // dst[i] = src[(i - n) mod 16] within each row
+  for (int l = 0; l < 64; ++l) out[l] = in[(l & ~15) | (((l & 15) - n) & 15)];
+}
+static void lane_xor(const Wave in, Wave out, int m) {
+  for (int l = 0; l < 64; ++l) out[l] = in[l ^ m];
+}
+
+struct Piece { uint32_t d[4]; };
+
+// One 4 KiB row: pieces[b][L] (already masked).  Returns per-lane s after the
+// chain (lane' layout).
+static void row_chain(Piece P[4][64], Wave s_out) {
+  static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
+  // exchange (x,y) with partner lane ^ X, c = lane bit
+  auto exch = [&](int sx, int sy, int X) {
+    for (int d = 0; d < 4; ++d) {
+      Wave send, recv;
+      for (int l = 0; l < 64; ++l) {
+        bool c = (l & X) != 0;
+        send[l] = c ? P[sx][l].d[d] : P[sy][l].d[d];
+      }
+      quad_perm(send, recv, X == 1 ? px1 : px2);
+      for (int l = 0; l < 64; ++l) {
+        bool c = (l & X) != 0;
+        uint32_t nx = c ? recv[l] : P[sx][l].d[d];
+        uint32_t ny = c ? P[sy][l].d[d] : recv[l];
+        P[sx][l].d[d] = nx;
+        P[sy][l].d[d] = ny;
+      }
+    }
+  };
+  exch(0, 1, 1);
+  exch(2, 3, 1);
+  exch(0, 2, 2);
+  exch(1, 3, 2);
+  for (int l = 0; l < 64; ++l) {
+    uint32_t lane4 = (uint32_t)(l & 31) * 4u, lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);
+    uint32_t x = P[0][l].d[0];
+    for (int k = 0; k < 4; ++k)
+      for (int d = 0; d < 4; ++d) {
+        if (!k && !d) continue;
+        x = slice4(x, lsel) ^ P[k][l].d[d];
+      }
+    s_out[l] = slice4(x, lsel);
+  }
+}
+
+static void mask_piece(Piece &p, int64_t v, int64_t len) {
+  for (int d = 0; d < 4; ++d) {
+    int64_t lo = v + 4 * d;
+    uint32_t m = 0xFFFFFFFFu;
+    if (lo < 0) m = (lo <= -4) ? 0u : (m << (8 * (uint32_t)(-lo)));
+    int64_t over = lo + 4 - len;
+    if (over > 0) m &= (over >= 4) ? 0u : (0xFFFFFFFFu >> (8 * (uint32_t)over));
+    p.d[d] &= m;
+  }
+}
+static Piece load_piece(const uint8_t *p) {
+  if (((uintptr_t)p) & 15u) { fprintf(stderr, "misaligned load\n"); exit(3); }
+  Piece r;
+  memcpy(r.d, p, 16);
+  return r;
+}
+
+static uint32_t reduce_lo(Wave s) { // rows: ror4, ror8, xor16, xor32; returns lane-wise (in place)
+  Wave t;
+  row_ror(s, t, 4); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+  row_ror(s, t, 8); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+  lane_xor(s, t, 16); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+  lane_xor(s, t, 32); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+  return s[0];
+}
+
+static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
+  if (len == 0) return 0;
+  const uint32_t z = (uint32_t)(0u - (uint32_t)(uintptr_t)(p0 + len)) & 15u;
+  const uint64_t lp = (uint64_t)len + z;
+  const uint32_t nrows = (uint32_t)((lp + 4095) / 4096);
+  const uint32_t first = (uint32_t)(lp - (uint64_t)(nrows - 1) * 4096);
+  static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
+  uint32_t W = 0;
+  static Piece P[4][64];
+  for (uint32_t r = 0; r < nrows; ++r) {
+    int64_t rs = (int64_t)lp - (int64_t)(nrows - r) * 4096;
+    bool last = r + 1 == nrows;
+    for (int b = 0; b < 4; ++b)
+      for (int L = 0; L < 64; ++L) {
+        int64_t v = rs + b * 1024 + 16 * L;
+        P[b][L] = (v + 16 > 0) ? load_piece(p0 + v) : Piece{{0, 0, 0, 0}};
+        if (rs < 0 || (last && z)) mask_piece(P[b][L], v, len);
+      }
+    Wave s, t;
+    row_chain(P, s);
+    for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsSH + (uint32_t)(l & 31) * 4u, 2048, 7);
+    quad_perm(s, t, px1); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+    quad_perm(s, t, px2); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+    for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsSL + (uint32_t)(l >> 2) * 4u, 1024, 6);
+    uint32_t rowcrc = reduce_lo(s);
+    for (int l = 1; l < 64; ++l) if (s[l] != rowcrc) { fprintf(stderr, "reduction not uniform\n"); exit(4); }
+    W = (r == 0) ? g_tq[first] : nib_map(W, kLdsRW2, 64, 2);
+    W ^= rowcrc;
+  }
+  if (z) W = nib_map(W, kLdsZI2 + (z - 1) * 512, 64, 2);
+  return ~W;
+}
+
+// Four items (<= 1 KiB each incl. end pad) in one row; returns 4 CRCs.
+static void emu_qb4(const uint8_t *const p0[4], const uint32_t len[4], int nvalid, uint32_t out[4]) {
+  static Piece P[4][64];
+  uint32_t z[4], w0[4];
+  for (int b = 0; b < 4; ++b) {
+    uint32_t L = b < nvalid ? len[b] : 0;
+    const uint8_t *q = b < nvalid ? p0[b] : p0[0];
+    z[b] = (uint32_t)(0u - (uint32_t)(uintptr_t)(q + L)) & 15u;
+    int64_t vstart = (int64_t)L + z[b] - 1024;
+    w0[b] = L == 0 ? 0u : g_tq[L + z[b]];
+    for (int Ln = 0; Ln < 64; ++Ln) {
+      int64_t v = vstart + 16 * Ln;
+      P[b][Ln] = (b < nvalid && L != 0 && v + 16 > 0) ? load_piece(q + v) : Piece{{0, 0, 0, 0}};
+      if (vstart < 0 || z[b]) mask_piece(P[b][Ln], v, L);
+    }
+  }
+  Wave s;
+  row_chain(P, s);
+  for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsSL + (uint32_t)(l >> 2) * 4u, 1024, 6);
+  reduce_lo(s);
+  for (int h = 0; h < 4; ++h) {
+    uint32_t res = w0[h] ^ s[h];
+    if (z[h]) res = nib_map(res, kLdsZI2 + (z[h] - 1) * 512, 64, 2);
+    res = ~res;
+    if (h >= nvalid || len[h] == 0) res = 0;
+    out[h] = res;
+  }
+}
+
+int main() {
+  int QB, mis;
+  unsigned long n;
+  if (scanf("%d %d %lu", &QB, &mis, &n) != 3) return 1;
+  std::vector<uint32_t> lens(n);
+  uint64_t total = 0;
+  for (unsigned long i = 0; i < n; ++i) {
+    if (scanf("%u", &lens[i]) != 1) return 1;
+    total += lens[i];
+  }
+  g_img.resize(kLdsBytesV2 / 4);
+  build_lds_image_v2(g_img.data());
+  g_tq.resize(kTqEntries);
+  build_tq(g_tq.data());
+  // guard bands: loads may touch the 16-B blocks around a body, never further
+  std::vector<uint8_t> raw(total + mis + 8192);
+  uint8_t *buf = raw.data() + 4096;
+  while ((uintptr_t)buf & 15u) ++buf;
+  auto mix = [](uint64_t zz) {
+    zz = (zz ^ (zz >> 30)) * 0xBF58476D1CE4E5B9ull;
+    zz = (zz ^ (zz >> 27)) * 0x94D049BB133111EBull;
+    return zz ^ (zz >> 31);
+  };
+  for (uint64_t i = 0; i < total + mis; ++i) {
+    uint64_t w = mix(7 + (i / 8 + 1) * 0x9E3779B97F4A7C15ull);
+    buf[i] = (uint8_t)(w >> (8 * (i % 8)));
+  }
+  std::vector<const uint8_t *> ptr(n);
+  uint64_t off = (uint64_t)mis;
+  for (unsigned long i = 0; i < n; ++i) {
+    ptr[i] = buf + off;
+    off += lens[i];
+  }
+  if (QB == 1) {
+    for (unsigned long i = 0; i < n; ++i) printf("%08x\n", emu_qb1(ptr[i], lens[i]));
+  } else {
+    for (unsigned long g = 0; g < n; g += 4) {
+      int nv = (int)((n - g) < 4 ? n - g : 4);
+      const uint8_t *pp[4];
+      uint32_t ll[4], out[4];
+      for (int b = 0; b < 4; ++b) {
+        pp[b] = b < nv ? ptr[g + b] : ptr[g];
+        ll[b] = b < nv ? lens[g + b] : 0;
+      }
+      emu_qb4(pp, ll, nv, out);
+      for (int b = 0; b < nv; ++b) printf("%08x\n", out[b]);
+    }
+  }
+  return 0;
+}

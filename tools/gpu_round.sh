@@ -1,0 +1,40 @@
+#!/bin/bash
+# tools/gpu_round.sh -- the GPU-box sequence: smoke, GPU tests, bench, probe,
+# rocprofv3 kernel-trace.  Each GPU step has its own time limit; after a fault,
+# abort or timeout (exit >= 124 or signal) nothing further touches the GPU.
+# Usage: bash tools/gpu_round.sh [tag] [steps...]   (steps: smoke tests bench probe prof pmc)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r01}; shift || true
+STEPS=${*:-"smoke tests bench probe prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+run() { # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "FATAL step $name rc=$rc; stopping"; exit $rc; fi
+  return $rc
+}
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
+    bench) run bench 600 python bench.py ;;
+    probe) run probe 600 python tools/probe.py ;;
+    ablate) run ablate 600 python tools/probe.py --mode ablate --rounds 3 ;;
+    counters) run counters 120 rocprofv3 -L ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+               python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive &&
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive ;;
+    *) python3 -c "print('unknown step $s')";;
+  esac
+done
+echo done

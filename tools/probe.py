@@ -2,15 +2,22 @@
 """tools/probe.py -- one-process A/B timing of kernel variants on one GPU
 (interleaved rounds, median; cdna_hip_programming.md 5.4 rule 24).
 
-  python tools/probe.py [--config ns] [--rounds 5] [--reps 10]
-Prints one JSON line per variant: stream-read patterns and CRC kernel options.
+  python tools/probe.py [--config ns] [--rounds 5] [--reps 10] [--mode lib|ablate]
+mode lib:    stream-read patterns and the product kernel under its runtime options.
+mode ablate: tools/libprobe.so variants (ABL bits: 1 no-compute, 2 no-combine,
+             4 no-load; DEPTH rows in flight; NT loads).  Ablated outputs are
+             wrong by construction -- timing only; abl=0 outputs are checked
+             against the product kernel.
 """
 import argparse
+import ctypes
 import json
 import os
 import statistics
+import subprocess
 import sys
 
+import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -31,24 +38,63 @@ def timed(fn, reps):
     return e0.elapsed_time(e1) / 1e3 / reps
 
 
+def lib_variants(w, a):
+    nbytes = (w.total // 4096) * 4096
+    v = {}
+    for pat in (0, 1):
+        for nt in (0, 1):
+            v[f"stream_read_p{pat}_nt{nt}"] = (lambda pat=pat, nt=nt: rpc_amd.stream_read(
+                w.base, pat, bool(nt), nbytes=nbytes), nbytes, None)
+    for nt in (0, 1):
+        for g in [int(x) for x in a.grids.split(",")]:
+            v[f"crc_nt{nt}_grid{g}"] = (w.step, w.algo_bytes, (nt, g))
+    return v
+
+
+def ablate_variants(w, a):
+    so = os.path.join(REPO, "tools", "libprobe.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tools")], check=True)
+    lib = ctypes.CDLL(so)
+    lib.probe_uniform.restype = ctypes.c_int
+    lib.probe_uniform.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p] + \
+        [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    out = torch.empty(w.n, dtype=torch.int32, device=w.device)
+    blocks = 256
+
+    def mk(nt, abl, depth):
+        def f():
+            rc = lib.probe_uniform(w.base.data_ptr(), w.n, w.L, out.data_ptr(), nt, abl, depth, blocks,
+                                   torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, rc
+        return f
+    v = {}
+    for nt in (0, 1):
+        for depth in (1, 2):
+            for abl in (0, 1, 2, 3, 4, 6):
+                v[f"abl{abl}_d{depth}_nt{nt}"] = (mk(nt, abl, depth), w.algo_bytes, None)
+    # correctness of the non-ablated probe builds vs the product kernel
+    w.step()
+    ref = w.out.clone()
+    for nt in (0, 1):
+        for depth in (1, 2):
+            mk(nt, 0, depth)()
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), (nt, depth)
+    return v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="ns")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--grids", default="0,512,1024")
+    ap.add_argument("--mode", default="lib", choices=["lib", "ablate"])
     a = ap.parse_args()
     torch.cuda.set_device(0)
     w = Workload(a.config, 0, torch.device("cuda", 0))
-    nbytes = (w.total // 4096) * 4096
-    variants = {}
-    for pat in (0, 1):
-        for nt in (0, 1):
-            variants[f"stream_read_p{pat}_nt{nt}"] = (lambda pat=pat, nt=nt: rpc_amd.stream_read(
-                w.base, pat, bool(nt), nbytes=nbytes), nbytes, None)
-    for nt in (0, 1):
-        for g in [int(x) for x in a.grids.split(",")]:
-            variants[f"crc_nt{nt}_grid{g}"] = (w.step, w.algo_bytes, (nt, g))
+    variants = lib_variants(w, a) if a.mode == "lib" else ablate_variants(w, a)
     res = {k: [] for k in variants}
     for _ in range(a.rounds):
         for k, (fn, nb, opt) in variants.items():
