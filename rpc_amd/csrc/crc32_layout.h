@@ -30,24 +30,25 @@ constexpr uint32_t kLdsS2 = kLdsS1 + 16384;  // 147456
 constexpr uint32_t kLdsRW = kLdsS2 + 4096;   // 151552
 constexpr uint32_t kLdsZI = kLdsRW + 512;    // 152064
 constexpr uint32_t kLdsBytes = kLdsZI + 15 * 512; // 159744 (156 KiB), v1 image
-constexpr uint32_t kLdsBytesV2 = 163840;          // v2 image (160 KiB)
+constexpr uint32_t kLdsBytesV2 = 157696;          // rows-kernel image (154 KiB)
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
 constexpr uint32_t kMaxRow = 64 * kSegBytes; // 4096
 constexpr uint32_t kTqEntries = kMaxRow + 1; // Tq[q] = A_q(0xFFFFFFFF), q=0..4096
 
 constexpr uint32_t row_bytes(int G) { return (uint32_t)G * kSegBytes; }
 
-// ---- v2 image (crc32_rows.h): main tables as above, then
-//   SH  16 KiB  SH[n][nib][c]  = A_{1024*(3-(c&3))}(nib << 4n), c = lane & 31
-//   SL   8 KiB  SL[n][nib][lo] = A_{64*(15-lo)}(nib << 4n),     lo = lane >> 2
-//   RW  512 B   RW[n][nib]     = A_4096(nib << 4n)
+// ---- rows-kernel image (crc32_rows.h): main tables as above, then
+//   ST1 16 KiB  ST1[n][nib][c]  = A_{64*(15-(c&15))}(nib << 4n), c = lane & 31
+//   ST2  2 KiB  ST2[n][nib][hi] = A_{1024*(3-hi)}(nib << 4n),    hi = 0..3
+//   RW  512 B   RW[n][nib]      = A_4096(nib << 4n)
 //   ZI  7.5 KiB ZI[z-1][n][nib] = A_z^-1(nib << 4n)
-constexpr uint32_t kLdsSH = 131072;
-constexpr uint32_t kLdsSL = kLdsSH + 16384;  // 147456
-constexpr uint32_t kLdsRW2 = kLdsSL + 8192;  // 155648
-constexpr uint32_t kLdsZI2 = kLdsRW2 + 512;  // 156160
-static_assert(kLdsZI2 + 15 * 512 == 163840, "v2 image fills the 160 KiB LDS exactly");
-void build_lds_image_v2(uint32_t *img /* 163840 bytes */);
+constexpr uint32_t kLdsST1 = 131072;
+constexpr uint32_t kLdsST2 = kLdsST1 + 16384; // 147456
+constexpr uint32_t kLdsRW2 = kLdsST2 + 2048;  // 149504
+constexpr uint32_t kLdsZI2 = kLdsRW2 + 512;   // 150016
+static_assert(kLdsZI2 + 15 * 512 == kLdsBytesV2, "rows image size");
+static_assert(kLdsBytesV2 % 16 == 0 && kLdsBytesV2 <= 163840, "fits the 160 KiB LDS");
+void build_lds_image_v2(uint32_t *img /* kLdsBytesV2 bytes */);
 
 // Host-side builders (crc32_tables.cpp).
 void build_lds_image(int G, uint32_t *img /* kLdsWords */);

@@ -83,15 +83,15 @@ void build_lds_image_v2(uint32_t *img) {
     }
   }
   uint32_t nt[8][16];
-  for (uint32_t c = 0; c < 32; ++c) { // hi = c & 3
-    nibble_table(1024u * (3u - (c & 3u)), nt);
+  for (uint32_t c = 0; c < 32; ++c) { // lo = c & 15
+    nibble_table(64u * (15u - (c & 15u)), nt);
     for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsSH + n * 2048 + nib * 128 + c * 4, nt[n][nib]);
+      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsST1 + n * 2048 + nib * 128 + c * 4, nt[n][nib]);
   }
-  for (uint32_t lo = 0; lo < 16; ++lo) {
-    nibble_table(64u * (15u - lo), nt);
+  for (uint32_t hi = 0; hi < 4; ++hi) {
+    nibble_table(1024u * (3u - hi), nt);
     for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsSL + n * 1024 + nib * 64 + lo * 4, nt[n][nib]);
+      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsST2 + n * 256 + nib * 16 + hi * 4, nt[n][nib]);
   }
   nibble_table(4096u, nt);
   for (int n = 0; n < 8; ++n)

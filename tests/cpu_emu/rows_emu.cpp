@@ -1,7 +1,7 @@
-// tests/cpu_emu/rows_emu.cpp -- CPU emulation of crc32_rows_kernel (v2) lane by
-// lane (TEST CODE): coalesced piece loads, the DPP lane-pair transpose, the
-// slice-by-4 chain on the v2 LDS image, SH/SL nibble steps with the exact DPP /
-// swizzle reduction patterns, Horner, Tq, ZI.  Compared with the oracle by
+// tests/cpu_emu/rows_emu.cpp -- CPU emulation of crc32_rows_kernel lane by lane
+// (TEST CODE): permuted coalesced piece loads, the v_permlane16/32_swap
+// transpose, the slice-by-4 chain on the rows LDS image, ST1/ST2 nibble steps
+// with the exact DPP quad/row_ror and permlane-swap reductions, Horner, Tq, ZI.  Compared with the oracle by
 // tests/test_kernel_emu.py.  Not the product path.
 //
 // stdin:  QB misalign n  then n lengths; bodies are splitmix bytes (seed 7)
@@ -55,32 +55,38 @@ static void lane_xor(const Wave in, Wave out, int m) {
 
 struct Piece { uint32_t d[4]; };
 
-// One 4 KiB row: pieces[b][L] (already masked).  Returns per-lane s after the
-// chain (lane' layout).
+static uint32_t piece_of_lane(uint32_t L) { return ((L & 15u) << 2) | (L >> 4); }
+
+// v_permlane16_swap vdst, vsrc: odd rows of vdst <-> even rows of vsrc.
+static void permlane16_swap(Wave x, Wave y) {
+  Wave nx, ny;
+  for (int l = 0; l < 64; ++l) { nx[l] = x[l]; ny[l] = y[l]; }
+  for (int l = 0; l < 64; ++l) {
+    if ((l >> 4) & 1) nx[l] = y[l - 16];   // odd row of vdst <- even row of vsrc
+    else ny[l] = x[l + 16];                // even row of vsrc <- odd row of vdst
+  }
+  for (int l = 0; l < 64; ++l) { x[l] = nx[l]; y[l] = ny[l]; }
+}
+// v_permlane32_swap vdst, vsrc: upper half of vdst <-> lower half of vsrc.
+static void permlane32_swap(Wave x, Wave y) {
+  Wave nx, ny;
+  for (int l = 0; l < 64; ++l) { nx[l] = x[l]; ny[l] = y[l]; }
+  for (int l = 0; l < 32; ++l) { nx[l + 32] = y[l]; ny[l] = x[l + 32]; }
+  for (int l = 0; l < 64; ++l) { x[l] = nx[l]; y[l] = ny[l]; }
+}
+
+// One 4 KiB row: P[b][lane] = the piece lane loaded in load b (already masked).
+// Returns the per-lane chain value after the transpose.
 static void row_chain(Piece P[4][64], Wave s_out) {
-  static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
-  // exchange (x,y) with partner lane ^ X, c = lane bit
-  auto exch = [&](int sx, int sy, int X) {
-    for (int d = 0; d < 4; ++d) {
-      Wave send, recv;
-      for (int l = 0; l < 64; ++l) {
-        bool c = (l & X) != 0;
-        send[l] = c ? P[sx][l].d[d] : P[sy][l].d[d];
-      }
-      quad_perm(send, recv, X == 1 ? px1 : px2);
-      for (int l = 0; l < 64; ++l) {
-        bool c = (l & X) != 0;
-        uint32_t nx = c ? recv[l] : P[sx][l].d[d];
-        uint32_t ny = c ? P[sy][l].d[d] : recv[l];
-        P[sx][l].d[d] = nx;
-        P[sy][l].d[d] = ny;
-      }
-    }
-  };
-  exch(0, 1, 1);
-  exch(2, 3, 1);
-  exch(0, 2, 2);
-  exch(1, 3, 2);
+  for (int d = 0; d < 4; ++d) {
+    Wave w[4];
+    for (int b = 0; b < 4; ++b) for (int l = 0; l < 64; ++l) w[b][l] = P[b][l].d[d];
+    permlane16_swap(w[0], w[1]);
+    permlane16_swap(w[2], w[3]);
+    permlane32_swap(w[0], w[2]);
+    permlane32_swap(w[1], w[3]);
+    for (int b = 0; b < 4; ++b) for (int l = 0; l < 64; ++l) P[b][l].d[d] = w[b][l];
+  }
   for (int l = 0; l < 64; ++l) {
     uint32_t lane4 = (uint32_t)(l & 31) * 4u, lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);
     uint32_t x = P[0][l].d[0];
@@ -91,6 +97,24 @@ static void row_chain(Piece P[4][64], Wave s_out) {
       }
     s_out[l] = slice4(x, lsel);
   }
+}
+
+static void xor_lanebit(Wave s, int bit) {
+  Wave a, b;
+  for (int l = 0; l < 64; ++l) { a[l] = s[l]; b[l] = s[l]; }
+  if (bit == 4) permlane16_swap(a, b); else permlane32_swap(a, b);
+  for (int l = 0; l < 64; ++l) s[l] = a[l] ^ b[l];
+}
+
+// ST1 step + reduce over lane bits 0-3 (quad_perm xor1, xor2, row_ror 4, 8).
+static void merge_lo(Wave s) {
+  static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
+  Wave t;
+  for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsST1 + (uint32_t)(l & 31) * 4u, 2048, 7);
+  quad_perm(s, t, px1); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+  quad_perm(s, t, px2); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+  row_ror(s, t, 4); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
+  row_ror(s, t, 8); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
 }
 
 static void mask_piece(Piece &p, int64_t v, int64_t len) {
@@ -110,22 +134,12 @@ static Piece load_piece(const uint8_t *p) {
   return r;
 }
 
-static uint32_t reduce_lo(Wave s) { // rows: ror4, ror8, xor16, xor32; returns lane-wise (in place)
-  Wave t;
-  row_ror(s, t, 4); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
-  row_ror(s, t, 8); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
-  lane_xor(s, t, 16); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
-  lane_xor(s, t, 32); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
-  return s[0];
-}
-
 static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
   if (len == 0) return 0;
   const uint32_t z = (uint32_t)(0u - (uint32_t)(uintptr_t)(p0 + len)) & 15u;
   const uint64_t lp = (uint64_t)len + z;
   const uint32_t nrows = (uint32_t)((lp + 4095) / 4096);
   const uint32_t first = (uint32_t)(lp - (uint64_t)(nrows - 1) * 4096);
-  static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
   uint32_t W = 0;
   static Piece P[4][64];
   for (uint32_t r = 0; r < nrows; ++r) {
@@ -133,17 +147,17 @@ static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
     bool last = r + 1 == nrows;
     for (int b = 0; b < 4; ++b)
       for (int L = 0; L < 64; ++L) {
-        int64_t v = rs + b * 1024 + 16 * L;
+        int64_t v = rs + b * 1024 + 16 * (int64_t)piece_of_lane((uint32_t)L);
         P[b][L] = (v + 16 > 0) ? load_piece(p0 + v) : Piece{{0, 0, 0, 0}};
         if (rs < 0 || (last && z)) mask_piece(P[b][L], v, len);
       }
-    Wave s, t;
+    Wave s;
     row_chain(P, s);
-    for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsSH + (uint32_t)(l & 31) * 4u, 2048, 7);
-    quad_perm(s, t, px1); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
-    quad_perm(s, t, px2); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
-    for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsSL + (uint32_t)(l >> 2) * 4u, 1024, 6);
-    uint32_t rowcrc = reduce_lo(s);
+    merge_lo(s);
+    for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsST2 + (uint32_t)(l >> 4) * 4u, 256, 4);
+    xor_lanebit(s, 4);
+    xor_lanebit(s, 5);
+    uint32_t rowcrc = s[0];
     for (int l = 1; l < 64; ++l) if (s[l] != rowcrc) { fprintf(stderr, "reduction not uniform\n"); exit(4); }
     W = (r == 0) ? g_tq[first] : nib_map(W, kLdsRW2, 64, 2);
     W ^= rowcrc;
@@ -163,17 +177,18 @@ static void emu_qb4(const uint8_t *const p0[4], const uint32_t len[4], int nvali
     int64_t vstart = (int64_t)L + z[b] - 1024;
     w0[b] = L == 0 ? 0u : g_tq[L + z[b]];
     for (int Ln = 0; Ln < 64; ++Ln) {
-      int64_t v = vstart + 16 * Ln;
+      int64_t v = vstart + 16 * (int64_t)piece_of_lane((uint32_t)Ln);
       P[b][Ln] = (b < nvalid && L != 0 && v + 16 > 0) ? load_piece(q + v) : Piece{{0, 0, 0, 0}};
       if (vstart < 0 || z[b]) mask_piece(P[b][Ln], v, L);
     }
   }
   Wave s;
   row_chain(P, s);
-  for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsSL + (uint32_t)(l >> 2) * 4u, 1024, 6);
-  reduce_lo(s);
+  merge_lo(s);
   for (int h = 0; h < 4; ++h) {
-    uint32_t res = w0[h] ^ s[h];
+    for (int l = 16 * h; l < 16 * h + 16; ++l)
+      if (s[l] != s[16 * h]) { fprintf(stderr, "row not uniform\n"); exit(4); }
+    uint32_t res = w0[h] ^ s[16 * h];
     if (z[h]) res = nib_map(res, kLdsZI2 + (z[h] - 1) * 512, 64, 2);
     res = ~res;
     if (h >= nvalid || len[h] == 0) res = 0;

@@ -27,6 +27,10 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py ;;
     probe) run probe 600 python tools/probe.py ;;
     ablate) run ablate 600 python tools/probe.py --mode ablate --rounds 3 ;;
+    ablate_c1) run ablate_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 ;;
+    bench_c1) run bench_c1 600 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive ;;
+    bench_c2) run bench_c2 600 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive ;;
+    bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive ;;

@@ -52,35 +52,38 @@ def lib_variants(w, a):
 
 
 def ablate_variants(w, a):
+    """Rows-kernel variants: (qb, pair, nt, abl) -- abl bits 1 no-compute,
+    2 no-merge, 4 no-load."""
     so = os.path.join(REPO, "tools", "libprobe.so")
     if not os.path.exists(so):
         subprocess.run(["make", "-C", os.path.join(REPO, "tools")], check=True)
     lib = ctypes.CDLL(so)
-    lib.probe_uniform.restype = ctypes.c_int
-    lib.probe_uniform.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p] + \
-        [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    lib.probe_rows.restype = ctypes.c_int
+    lib.probe_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                               ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
     out = torch.empty(w.n, dtype=torch.int32, device=w.device)
     blocks = 256
 
-    def mk(nt, abl, depth):
+    def mk(qb, pair, nt, abl):
         def f():
-            rc = lib.probe_uniform(w.base.data_ptr(), w.n, w.L, out.data_ptr(), nt, abl, depth, blocks,
-                                   torch.cuda.current_stream().cuda_stream)
-            assert rc == 0, rc
+            rc = lib.probe_rows(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, pair, nt, abl, blocks,
+                                torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, (qb, pair, nt, abl, rc)
         return f
-    v = {}
-    for nt in (0, 1):
-        for depth in (1, 2):
-            for abl in (0, 1, 2, 3, 4, 6):
-                v[f"abl{abl}_d{depth}_nt{nt}"] = (mk(nt, abl, depth), w.algo_bytes, None)
-    # correctness of the non-ablated probe builds vs the product kernel
+    combos = [(1, 2, 1, 0), (1, 2, 0, 0), (1, 1, 1, 0), (1, 1, 0, 0), (1, 2, 1, 3), (1, 2, 1, 4), (1, 2, 1, 6),
+              (1, 2, 1, 1), (1, 2, 1, 2), (1, 1, 1, 3), (1, 1, 1, 4), (1, 1, 1, 6)]
+    if w.L <= 1024:  # aligned uniform bodies: z = 0
+        combos += [(4, 1, 1, 0), (4, 1, 0, 0), (4, 2, 1, 0), (4, 2, 0, 0), (4, 1, 1, 4), (4, 2, 1, 4)]
+    v = {f"qb{qb}_pair{p}_nt{nt}_abl{abl}": (mk(qb, p, nt, abl), w.algo_bytes, None) for qb, p, nt, abl in combos}
+    # correctness of every non-ablated variant vs the product kernel
     w.step()
+    torch.cuda.synchronize()
     ref = w.out.clone()
-    for nt in (0, 1):
-        for depth in (1, 2):
-            mk(nt, 0, depth)()
+    for qb, p, nt, abl in combos:
+        if abl == 0:
+            mk(qb, p, nt, 0)()
             torch.cuda.synchronize()
-            assert torch.equal(out, ref), (nt, depth)
+            assert torch.equal(out, ref), (qb, p, nt)
     return v
 
 
