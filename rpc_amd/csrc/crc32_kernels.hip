@@ -124,24 +124,23 @@ static constexpr int kBlock = 1024;
 
 hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream) {
   if (a.n_items == 0) return hipSuccess;
-  // QB = 1: two rows per step (PAIR = 2), 12-wave workgroups.
-  // QB = 4: one 4-item row per step (PAIR = 1), 16-wave workgroups.
-  const int waves_per_block = (QB == 4) ? 16 : 12;
-  const uint64_t per_wave = (QB == 4) ? 4 : 2;
+  // One row per step (PAIR = 1), 16-wave (1024-thread) workgroups, one per CU.
+  constexpr int kWaves = 16;
+  const uint64_t per_wave = (QB == 4) ? 4 : 1;
   const uint64_t waves = (a.n_items + per_wave - 1) / per_wave;
-  uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
+  uint64_t blocks = (waves + kWaves - 1) / kWaves;
   if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
-  const dim3 grid((unsigned)blocks), block(waves_per_block * 64);
+  const dim3 grid((unsigned)blocks), block(kWaves * 64);
   if (QB == 4) {
     if (nt)
-      hipLaunchKernelGGL((crc32_rows_kernel<4, true, 1>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((crc32_rows_kernel<4, true>), grid, block, 0, stream, a);
     else
-      hipLaunchKernelGGL((crc32_rows_kernel<4, false, 1>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((crc32_rows_kernel<4, false>), grid, block, 0, stream, a);
   } else {
     if (nt)
-      hipLaunchKernelGGL((crc32_rows_kernel<1, true, 2>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((crc32_rows_kernel<1, true>), grid, block, 0, stream, a);
     else
-      hipLaunchKernelGGL((crc32_rows_kernel<1, false, 2>), grid, block, 0, stream, a);
+      hipLaunchKernelGGL((crc32_rows_kernel<1, false>), grid, block, 0, stream, a);
   }
   return hipGetLastError();
 }

@@ -30,7 +30,7 @@ constexpr uint32_t kLdsS2 = kLdsS1 + 16384;  // 147456
 constexpr uint32_t kLdsRW = kLdsS2 + 4096;   // 151552
 constexpr uint32_t kLdsZI = kLdsRW + 512;    // 152064
 constexpr uint32_t kLdsBytes = kLdsZI + 15 * 512; // 159744 (156 KiB), v1 image
-constexpr uint32_t kLdsBytesV2 = 157696;          // rows-kernel image (154 KiB)
+constexpr uint32_t kLdsBytesV2 = 158736;          // rows-kernel image (155 KiB)
 constexpr uint32_t kLdsWords = kLdsBytes / 4;
 constexpr uint32_t kMaxRow = 64 * kSegBytes; // 4096
 constexpr uint32_t kTqEntries = kMaxRow + 1; // Tq[q] = A_q(0xFFFFFFFF), q=0..4096
@@ -42,11 +42,15 @@ constexpr uint32_t row_bytes(int G) { return (uint32_t)G * kSegBytes; }
 //   ST2  2 KiB  ST2[n][nib][hi] = A_{1024*(3-hi)}(nib << 4n),    hi = 0..3
 //   RW  512 B   RW[n][nib]      = A_4096(nib << 4n)
 //   ZI  7.5 KiB ZI[z-1][n][nib] = A_z^-1(nib << 4n)
+//   TQ16 1 KiB  TQ16[k]         = A_{16k}(0xFFFFFFFF), k = 0..256
 constexpr uint32_t kLdsST1 = 131072;
 constexpr uint32_t kLdsST2 = kLdsST1 + 16384; // 147456
 constexpr uint32_t kLdsRW2 = kLdsST2 + 2048;  // 149504
 constexpr uint32_t kLdsZI2 = kLdsRW2 + 512;   // 150016
-static_assert(kLdsZI2 + 15 * 512 == kLdsBytesV2, "rows image size");
+// TQ16[k] = A_{16k}(0xFFFFFFFF), k = 0..256: zlib pre-conditioning seeds for
+// first rows of 16k bytes (other lengths: round up, undo with ZI).
+constexpr uint32_t kLdsTQ16 = kLdsZI2 + 15 * 512; // 157696
+static_assert(kLdsTQ16 + 1040 == kLdsBytesV2, "rows image size");
 static_assert(kLdsBytesV2 % 16 == 0 && kLdsBytesV2 <= 163840, "fits the 160 KiB LDS");
 void build_lds_image_v2(uint32_t *img /* kLdsBytesV2 bytes */);
 

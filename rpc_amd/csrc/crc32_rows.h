@@ -98,9 +98,12 @@ __device__ __forceinline__ uint32_t shfl_xor32(uint32_t v) {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// 16-byte global load.  The pointer is cast to the global address space so a
+// selected / integer-derived address still compiles to global_load (in-order
+// vmcnt accounting) rather than flat_load (which also ties up lgkmcnt).
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
-  const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+  const __attribute__((address_space(1))) u32x4 *q = (const __attribute__((address_space(1))) u32x4 *)(p);
   if constexpr (NT)
     return __builtin_nontemporal_load(q);
   else
@@ -175,17 +178,23 @@ __device__ __forceinline__ uint32_t seg_crc(const uint8_t *lds, const u32x4 (&p)
   return slice4(lds, x, lsel);
 }
 
-struct RowTask {
-  const uint8_t *p0; // item start
-  uint64_t item;
-  uint64_t lp;       // len + z (end 16-byte aligned)
-  uint32_t len;
-  uint32_t nrows;
-  uint32_t r;
-  uint32_t z;
-  uint32_t w0;
-  uint32_t valid;
-};
+// Read-only kernel inputs through the constant address space: uniform indices
+// then compile to scalar loads (s_load, counted by lgkmcnt) instead of vector
+// loads that would sit in the vmcnt queue in front of the row prefetch.
+template <typename T>
+__device__ __forceinline__ T ld_const(const T *p, uint64_t i) {
+  return ((const __attribute__((address_space(4))) T *)(p))[i];
+}
+
+// A_first(0xFFFFFFFF), the zlib pre-conditioning seed for a first row of
+// `first` bytes: TQ16 holds multiples of 16; other lengths round up and undo
+// the extra bytes with the ZI inverse-shift tables.
+__device__ __forceinline__ uint32_t seed_for(const uint8_t *lds, uint32_t first) {
+  const uint32_t up = (first + 15u) & ~15u;
+  uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
+  if (up != first) w = nib_map<64u, 2u>(lds, w, kLdsZI2 + (up - first - 1u) * 512u);
+  return w;
+}
 
 } // namespace rows
 
@@ -195,24 +204,6 @@ constexpr int kRowsAblNoMerge = 2;   // skip the per-lane shift / reductions
 constexpr int kRowsAblNoLoad = 4;    // synthesize row data instead of loading it
 
 namespace rows {
-
-// Two independent chains interleaved step by step (2x LDS reads in flight).
-__device__ __forceinline__ void seg_crc2(const uint8_t *lds, const u32x4 (&p)[4], const u32x4 (&q)[4],
-                                         uint32_t lsel, uint32_t &s0, uint32_t &s1) {
-  uint32_t x = p[0][0], y = q[0][0];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      if (k == 0 && d == 0) continue;
-      const uint32_t nx = slice4w(lds, x, p[k][d], lsel);
-      const uint32_t ny = slice4w(lds, y, q[k][d], lsel);
-      x = nx;
-      y = ny;
-    }
-  s0 = slice4(lds, x, lsel);
-  s1 = slice4(lds, y, lsel);
-}
 
 __device__ __forceinline__ uint32_t xor_fold(const u32x4 (&p)[4]) {
   uint32_t r = 0;
@@ -238,37 +229,6 @@ __device__ __forceinline__ uint32_t merge(const uint8_t *lds, uint32_t s, uint32
   return s;
 }
 
-template <int QB>
-__device__ __forceinline__ void merge2(const uint8_t *lds, uint32_t &s0, uint32_t &s1, uint32_t st1_base,
-                                       uint32_t st2_base) {
-  s0 = nib_map<2048u, 7u>(lds, s0, st1_base);
-  s1 = nib_map<2048u, 7u>(lds, s1, st1_base);
-  s0 ^= dpp_xor1(s0);
-  s1 ^= dpp_xor1(s1);
-  s0 ^= dpp_xor2(s0);
-  s1 ^= dpp_xor2(s1);
-  s0 ^= dpp_ror4(s0);
-  s1 ^= dpp_ror4(s1);
-  s0 ^= dpp_ror8(s0);
-  s1 ^= dpp_ror8(s1);
-  if constexpr (QB == 1) {
-    s0 = nib_map<256u, 4u>(lds, s0, st2_base);
-    s1 = nib_map<256u, 4u>(lds, s1, st2_base);
-    s0 = xor_lanebit4(s0);
-    s1 = xor_lanebit4(s1);
-    s0 = xor_lanebit5(s0);
-    s1 = xor_lanebit5(s1);
-  }
-}
-
-// QB = 4 task: item group g = items [4g, 4g+4); quarter b <-> item 4g+b.  Only
-// the group index is carried; per-quarter facts are re-derived (scalar loads)
-// where needed, which keeps the task in a few SGPRs.
-struct QuadTask {
-  uint64_t g;
-  uint32_t nvalid; // valid items in the group (0..4); 0 = no task
-};
-
 struct QuarterInfo {
   const uint8_t *p0;
   uint32_t len;
@@ -279,11 +239,13 @@ struct QuarterInfo {
 } // namespace rows
 
 // QB = 1: rows of one item.  QB = 4: four items (<= 1 KiB each) per row.
-// PAIR = 2: two rows computed together (two interleaved lookup chains).
-// WAVES = wavefronts per (one-per-CU) workgroup; PAIR = 2 needs the larger
-// register budget of 12 waves (3 per SIMD).
-template <int QB, bool NT, int PAIR = 2, int ABL = 0, int WAVES = (PAIR == 2 ? 12 : 16)>
-__global__ void __launch_bounds__(WAVES * 64, WAVES / 4) crc32_rows_kernel(ItemsArgs a) {
+// One 1024-thread workgroup (16 waves) per CU; each wave walks its tasks with
+// one row of loads in flight ahead of the row it computes.  Every row issues
+// exactly 4 loads and 1 store so the compiler can count vmcnt exactly (the
+// prefetch is never drained early).  Per-task state is plain wave-uniform
+// scalars (SGPRs); item metadata comes from scalar loads.
+template <int QB, bool NT, int ABL = 0>
+__global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
   {
@@ -297,15 +259,15 @@ __global__ void __launch_bounds__(WAVES * 64, WAVES / 4) crc32_rows_kernel(Items
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t lane4 = (lane & 31u) * 4u;
   const uint32_t lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);
-  const uint32_t hi = lane >> 4;               // quarter / row of 16 lanes after the transpose
+  const uint32_t hi = lane >> 4;                   // 16-lane row = quarter after the transpose
   const uint32_t pofs = 16u * piece_of_lane(lane); // byte offset of this lane's piece in a quarter
   const uint32_t st1_base = kLdsST1 + lane4;
   const uint32_t st2_base = kLdsST2 + hi * 4u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
-  const uint64_t gw = (uint64_t)blockIdx.x * wpb + wave;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 16u;
+  const uint64_t gw = (uint64_t)blockIdx.x * 16u + wave;
   const uint32_t mode = a.mode;
+  const uint64_t n = a.n_items;
 
   auto synth = [&](uint64_t key, u32x4 (&buf)[4]) {
 #pragma unroll
@@ -314,230 +276,192 @@ __global__ void __launch_bounds__(WAVES * 64, WAVES / 4) crc32_rows_kernel(Items
       buf[b] = u32x4{v, v ^ 0x5bd1e995u, v + 0x68e31da4u, ~v};
     }
   };
-  auto chain1 = [&](const u32x4 (&buf)[4]) -> uint32_t {
-    if constexpr ((ABL & kRowsAblNoCompute) != 0) return xor_fold(buf);
-    else return seg_crc(lds, buf, lsel);
-  };
-  auto chain2 = [&](const u32x4 (&p)[4], const u32x4 (&q)[4], uint32_t &s0, uint32_t &s1) {
-    if constexpr ((ABL & kRowsAblNoCompute) != 0) {
-      s0 = xor_fold(p);
-      s1 = xor_fold(q);
-    } else {
-      seg_crc2(lds, p, q, lsel, s0, s1);
-    }
-  };
-  auto do_merge1 = [&](uint32_t s) -> uint32_t {
-    if constexpr ((ABL & kRowsAblNoMerge) != 0) return s;
-    else return merge<QB>(lds, s, st1_base, st2_base);
-  };
-  auto do_merge2 = [&](uint32_t &s0, uint32_t &s1) {
-    if constexpr ((ABL & kRowsAblNoMerge) == 0) merge2<QB>(lds, s0, s1, st1_base, st2_base);
+  auto row_crc = [&](u32x4 (&buf)[4]) -> uint32_t {
+    transpose(buf);
+    uint32_t s;
+    if constexpr ((ABL & kRowsAblNoCompute) != 0) s = xor_fold(buf);
+    else s = seg_crc(lds, buf, lsel);
+    if constexpr ((ABL & kRowsAblNoMerge) == 0) s = merge<QB>(lds, s, st1_base, st2_base);
+    return s;
   };
 
-  // ---- task policies ----------------------------------------------------------
-  // QB = 1
-  auto load_item = [&](uint64_t item, RowTask &t) {
-    for (;;) {
-      if (item >= a.n_items) {
-        t.valid = 0u;
-        return;
-      }
-      const uint64_t off = a.offsets ? a.offsets[item] : item * a.stride;
-      const uint32_t len = a.lengths ? a.lengths[item] : a.len;
-      if (len == 0) {
-        if (lane == 0) a.out[item] = 0u;
-        item += nwaves;
-        continue;
-      }
-      t.valid = 1u;
-      t.item = item;
-      t.p0 = a.base + off;
-      t.len = len;
-      t.z = (uint32_t)(0u - (uint32_t)(uintptr_t)(t.p0 + len)) & 15u;
-      t.lp = (uint64_t)len + t.z;
-      t.nrows = (uint32_t)((t.lp + kRow - 1) / kRow);
-      t.r = 0;
-      const uint32_t first = (uint32_t)(t.lp - (uint64_t)(t.nrows - 1) * kRow);
-      t.w0 = (mode == kModeRaw) ? 0u : a.tq[first];
-      return;
-    }
-  };
-  // QB = 4
-  const uint64_t ngroups = (a.n_items + 3) / 4;
-  auto load_group = [&](uint64_t g, QuadTask &q) {
-    q.g = g;
-    q.nvalid = 0;
-    if (g >= ngroups) return;
-    const uint64_t left = a.n_items - 4 * g;
-    q.nvalid = left >= 4 ? 4u : (uint32_t)left;
-  };
-  auto quarter = [&](const QuadTask &q, int b) -> QuarterInfo {
-    QuarterInfo r;
-    const uint64_t item = 4 * q.g + b;
-    const bool ok = (uint32_t)b < q.nvalid;
-    const uint64_t off = !ok ? 0 : a.offsets ? a.offsets[item] : item * a.stride;
-    r.len = !ok ? 0u : a.lengths ? a.lengths[item] : a.len;
-    r.p0 = a.base + off;
-    r.z = (uint32_t)(0u - (uint32_t)(uintptr_t)(r.p0 + r.len)) & 15u;
-    r.vstart = (int64_t)r.len + r.z - (int64_t)kQuarter;
-    return r;
-  };
-  using Task = typename std::conditional<QB == 1, RowTask, QuadTask>::type;
-  auto first_task = [&](Task &t) {
-    if constexpr (QB == 1) load_item(gw, t);
-    else load_group(gw, t);
-  };
-  auto valid = [&](const Task &t) -> bool {
-    if constexpr (QB == 1) return t.valid != 0u;
-    else return t.nvalid != 0u;
-  };
-  auto next_task = [&](const Task &c, Task &n) {
-    if constexpr (QB == 1) {
-      if (c.r + 1 < c.nrows) {
-        n = c;
-        n.r = c.r + 1;
+  if constexpr (QB == 1) {
+    // Item metadata (wave-uniform).  item must be < n.
+    auto meta = [&](uint64_t item, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &nr) {
+      const uint64_t off = a.offsets ? ld_const(a.offsets, item) : item * a.stride;
+      len = a.lengths ? ld_const(a.lengths, item) : a.len;
+      p0 = (uint64_t)(uintptr_t)a.base + off;
+      z = (uint32_t)(0u - (uint32_t)(p0 + len)) & 15u;
+      lp = (uint64_t)len + z;
+      const uint64_t rows_ = (lp + kRow - 1) / kRow;
+      nr = rows_ ? (uint32_t)rows_ : 1u; // zero-length items: one fully masked row
+    };
+    auto issue = [&](uint64_t p0, uint64_t lp, uint32_t nr, uint32_t r, bool ok, uint64_t safe, u32x4 (&buf)[4]) {
+      if constexpr ((ABL & kRowsAblNoLoad) != 0) {
+        synth(p0 + r, buf);
       } else {
-        load_item(c.item + nwaves, n);
-      }
-    } else {
-      load_group(c.g + nwaves, n);
-    }
-  };
-  auto row_start = [&](const RowTask &t) -> int64_t {
-    return (int64_t)t.lp - (int64_t)(t.nrows - t.r) * (int64_t)kRow;
-  };
-  auto issue = [&](const Task &t, u32x4 (&buf)[4]) {
-    if constexpr ((ABL & kRowsAblNoLoad) != 0) {
-      if constexpr (QB == 1) synth(t.item * 131u + t.r, buf);
-      else synth(t.g, buf);
-    } else if constexpr (QB == 1) {
-      const int64_t rs = row_start(t);
-      if (rs >= 0) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) buf[b] = ld16<NT>(t.p0 + rs + b * kQuarter + pofs);
-      } else {
+        const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           const int64_t v = rs + b * kQuarter + (int64_t)pofs;
-          buf[b] = (v + 16 > 0) ? ld16<NT>(t.p0 + v) : u32x4{0u, 0u, 0u, 0u};
+          const uint64_t src = (ok && v + 16 > 0) ? p0 + (uint64_t)v : safe;
+          buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
         }
       }
-    } else {
+    };
+    uint32_t W = 0;
+    // Finished CRCs are parked in one VGPR (lane k = this wave's k-th pending
+    // item, item = gw + (j0 + k) * nwaves) and stored 64 at a time: a per-row
+    // store would make the compiler drain vmcnt (store-data WAR) every row.
+    uint32_t outv = 0, ocount = 0;
+    uint64_t j0 = 0;
+    auto flush = [&]() {
+      if (lane < ocount) a.out[gw + (j0 + lane) * nwaves] = outv;
+      j0 += ocount;
+      ocount = 0;
+    };
+    auto park = [&](uint32_t res) {
+      outv = (lane == ocount) ? res : outv;
+      if (++ocount == 64u) flush();
+    };
+    auto compute = [&](uint64_t item, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r,
+                       u32x4 (&buf)[4]) {
+      const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
+      const bool last = r + 1 == nr;
+      if (rs < 0 || (last && z != 0)) {
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const QuarterInfo qi = quarter(t, b);
-        const int64_t v = qi.vstart + (int64_t)pofs;
-        buf[b] = (qi.len != 0 && v + 16 > 0) ? ld16<NT>(qi.p0 + v) : u32x4{0u, 0u, 0u, 0u};
+        for (int b = 0; b < 4; ++b) buf[b] = mask_piece(buf[b], rs + b * kQuarter + (int64_t)pofs, len);
       }
-    }
-  };
-  // mask + transpose
-  auto prep = [&](const Task &t, u32x4 (&buf)[4]) {
-    if constexpr (QB == 1) {
-      const int64_t rs = row_start(t);
-      if (rs < 0 || (t.r + 1 == t.nrows && t.z != 0)) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) buf[b] = mask_piece(buf[b], rs + b * kQuarter + (int64_t)pofs, t.len);
+      const uint32_t s = row_crc(buf);
+      if (r == 0) {
+        const uint32_t first = (uint32_t)(lp - (uint64_t)(nr - 1) * kRow);
+        W = (mode == kModeRaw) ? 0u : seed_for(lds, first);
+      } else {
+        W = nib_map<64u, 2u>(lds, W, kLdsRW2);
       }
-    } else {
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const QuarterInfo qi = quarter(t, b);
-        if (qi.vstart < 0 || qi.z != 0) buf[b] = mask_piece(buf[b], qi.vstart + (int64_t)pofs, qi.len);
-      }
-    }
-    transpose(buf);
-  };
-  uint32_t W = 0; // QB = 1 Horner accumulator (wave-uniform)
-  auto finish = [&](const Task &t, uint32_t s) {
-    if constexpr (QB == 1) {
-      W = (t.r == 0) ? t.w0 : nib_map<64u, 2u>(lds, W, kLdsRW2);
       W ^= s;
-      if (t.r + 1 == t.nrows) {
+      if (last) {
         uint32_t res = W;
-        if (t.z != 0) res = nib_map<64u, 2u>(lds, res, kLdsZI2 + (t.z - 1u) * 512u);
+        if (z != 0) res = nib_map<64u, 2u>(lds, res, kLdsZI2 + (z - 1u) * 512u);
         if (mode == kModeFinal) res = ~res;
-        if (lane == 0) a.out[t.item] = res;
+        park(res);
       }
-    } else {
+    };
+
+    uint64_t c_item = gw;
+    if (c_item >= n) return;
+    uint64_t c_p0, c_lp;
+    uint32_t c_len, c_z, c_nr, c_r = 0;
+    meta(c_item, c_p0, c_lp, c_len, c_z, c_nr);
+    const uint64_t safe = c_p0 & ~(uint64_t)15; // 16-B block holding this wave's first byte
+    u32x4 bufA[4], bufB[4];
+    issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
+    auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
+      const bool adv = c_r + 1 < c_nr;
+      const uint64_t n_item = adv ? c_item : c_item + nwaves;
+      const bool ok = n_item < n;
+      uint64_t m_p0, m_lp;
+      uint32_t m_len, m_z, m_nr;
+      meta(ok ? n_item : c_item, m_p0, m_lp, m_len, m_z, m_nr);
+      const uint32_t n_r = adv ? c_r + 1 : 0u;
+      issue(m_p0, m_lp, m_nr, n_r, ok, safe, nb);
+      compute(c_item, c_lp, c_len, c_z, c_nr, c_r, cb);
+      c_item = n_item;
+      c_r = n_r;
+      c_p0 = m_p0;
+      c_lp = m_lp;
+      c_len = m_len;
+      c_z = m_z;
+      c_nr = m_nr;
+      return ok;
+    };
+    for (;;) {
+      if (!step(bufA, bufB)) break;
+      if (!step(bufB, bufA)) break;
+    }
+    flush();
+  } else {
+    // QB = 4: group g = items [4g, 4g+4), quarter b <-> item 4g+b (len + pad <= 1 KiB).
+    const uint64_t ngroups = (n + 3) / 4;
+    auto quarter = [&](uint64_t g, int b) -> QuarterInfo {
+      QuarterInfo r;
+      const uint64_t item = 4 * g + b;
+      const bool ok = item < n;
+      const uint64_t it = ok ? item : 0;
+      const uint64_t off = a.offsets ? ld_const(a.offsets, it) : it * a.stride;
+      const uint32_t len = a.lengths ? ld_const(a.lengths, it) : a.len;
+      r.len = ok ? len : 0u;
+      r.p0 = a.base + off;
+      r.z = (uint32_t)(0u - (uint32_t)(uintptr_t)(r.p0 + r.len)) & 15u;
+      r.vstart = (int64_t)r.len + r.z - (int64_t)kQuarter;
+      return r;
+    };
+    auto issue = [&](uint64_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) {
+      if constexpr ((ABL & kRowsAblNoLoad) != 0) {
+        synth(g, buf);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const QuarterInfo qi = quarter(g, b);
+          const int64_t v = qi.vstart + (int64_t)pofs;
+          const uint64_t src = (ok && qi.len != 0 && v + 16 > 0) ? (uint64_t)(uintptr_t)qi.p0 + (uint64_t)v : safe;
+          buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
+        }
+      }
+    };
+    // Parked results: lane k = item 4*(gw + (j0 + k/4) * nwaves) + k%4 (see QB = 1).
+    uint32_t outv = 0, ocount = 0;
+    uint64_t j0 = 0;
+    auto flush = [&]() {
+      const uint64_t item = 4 * (gw + (j0 + lane / 4u) * nwaves) + (lane & 3u);
+      if (lane < ocount && item < n) a.out[item] = outv;
+      j0 += ocount / 4u;
+      ocount = 0;
+    };
+    auto compute = [&](uint64_t g, u32x4 (&buf)[4]) {
       uint32_t z = 0, len = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const QuarterInfo qi = quarter(t, b);
+        const QuarterInfo qi = quarter(g, b);
+        if (qi.vstart < 0 || qi.z != 0 || qi.len == 0)
+          buf[b] = mask_piece(buf[b], qi.vstart + (int64_t)pofs, qi.len);
         if (hi == (uint32_t)b) {
           z = qi.z;
           len = qi.len;
         }
       }
-      const uint32_t w0 = (mode == kModeRaw || len == 0) ? 0u : a.tq[len + z];
-      uint32_t res = w0 ^ s;
+      const uint32_t s = row_crc(buf); // lanes of 16-lane row b hold crc0 of item 4g+b
+      uint32_t res = (mode == kModeRaw) ? 0u : seed_for(lds, len + z);
+      res ^= s;
       if (z != 0) res = nib_map<64u, 2u>(lds, res, kLdsZI2 + (z - 1u) * 512u);
       if (mode == kModeFinal) res = ~res;
       if (len == 0) res = 0u;
-      if ((lane & 15u) == 0 && hi < t.nvalid) a.out[4 * t.g + hi] = res;
-    }
-  };
-
-  if constexpr (PAIR == 1) {
-    Task cur, nxt;
-    u32x4 bufA[4], bufB[4];
-    first_task(cur);
-    if (valid(cur)) issue(cur, bufA);
-    auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
-      next_task(cur, nxt);
-      if (valid(nxt)) issue(nxt, nb);
-      prep(cur, cb);
-      finish(cur, do_merge1(chain1(cb)));
-      cur = nxt;
-    };
-    for (;;) {
-      if (!valid(cur)) break;
-      step(bufA, bufB);
-      if (!valid(cur)) break;
-      step(bufB, bufA);
-    }
-  } else {
-    // Two rows per step; the next two rows load while these two compute.
-    Task c0, c1, n0, n1;
-    u32x4 A0[4], A1[4], B0[4], B1[4];
-    first_task(c0);
-    if (valid(c0)) {
-      issue(c0, A0);
-      next_task(c0, c1);
-      if (valid(c1)) issue(c1, A1);
-    } else {
-      c1 = c0;
-    }
-    auto step = [&](u32x4 (&p0)[4], u32x4 (&p1)[4], u32x4 (&q0)[4], u32x4 (&q1)[4]) {
-      if (valid(c1)) {
-        next_task(c1, n0);
-        if (valid(n0)) {
-          issue(n0, q0);
-          next_task(n0, n1);
-          if (valid(n1)) issue(n1, q1);
-        } else {
-          n1 = n0;
-        }
-      } else {
-        n0 = c1;
-        n1 = c1;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t v = __builtin_amdgcn_readlane(res, 16 * b);
+        outv = (lane == ocount + (uint32_t)b) ? v : outv;
       }
-      prep(c0, p0);
-      prep(c1, p1);
-      uint32_t s0, s1;
-      chain2(p0, p1, s0, s1);
-      do_merge2(s0, s1);
-      finish(c0, s0);
-      if (valid(c1)) finish(c1, s1);
-      c0 = n0;
-      c1 = n1;
+      ocount += 4;
+      if (ocount == 64u) flush();
+    };
+    uint64_t g = gw;
+    if (g >= ngroups) return;
+    const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
+    u32x4 bufA[4], bufB[4];
+    issue(g, true, safe, bufA);
+    auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
+      const uint64_t ng = g + nwaves;
+      const bool ok = ng < ngroups;
+      issue(ok ? ng : g, ok, safe, nb);
+      compute(g, cb);
+      g = ng;
+      return ok;
     };
     for (;;) {
-      if (!valid(c0)) break;
-      step(A0, A1, B0, B1);
-      if (!valid(c0)) break;
-      step(B0, B1, A0, A1);
+      if (!step(bufA, bufB)) break;
+      if (!step(bufB, bufA)) break;
     }
+    flush();
   }
 }
 

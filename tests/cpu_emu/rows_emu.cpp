@@ -55,6 +55,13 @@ static void lane_xor(const Wave in, Wave out, int m) {
 
 struct Piece { uint32_t d[4]; };
 
+static uint32_t seed_for(uint32_t first) {
+  uint32_t up = (first + 15u) & ~15u;
+  uint32_t w = ld(kLdsTQ16 + up / 4u);
+  if (up != first) w = nib_map(w, kLdsZI2 + (up - first - 1u) * 512u, 64, 2);
+  return w;
+}
+
 static uint32_t piece_of_lane(uint32_t L) { return ((L & 15u) << 2) | (L >> 4); }
 
 // v_permlane16_swap vdst, vsrc: odd rows of vdst <-> even rows of vsrc.
@@ -159,7 +166,7 @@ static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
     xor_lanebit(s, 5);
     uint32_t rowcrc = s[0];
     for (int l = 1; l < 64; ++l) if (s[l] != rowcrc) { fprintf(stderr, "reduction not uniform\n"); exit(4); }
-    W = (r == 0) ? g_tq[first] : nib_map(W, kLdsRW2, 64, 2);
+    W = (r == 0) ? seed_for(first) : nib_map(W, kLdsRW2, 64, 2);
     W ^= rowcrc;
   }
   if (z) W = nib_map(W, kLdsZI2 + (z - 1) * 512, 64, 2);
@@ -175,7 +182,7 @@ static void emu_qb4(const uint8_t *const p0[4], const uint32_t len[4], int nvali
     const uint8_t *q = b < nvalid ? p0[b] : p0[0];
     z[b] = (uint32_t)(0u - (uint32_t)(uintptr_t)(q + L)) & 15u;
     int64_t vstart = (int64_t)L + z[b] - 1024;
-    w0[b] = L == 0 ? 0u : g_tq[L + z[b]];
+    w0[b] = L == 0 ? 0u : seed_for(L + z[b]);
     for (int Ln = 0; Ln < 64; ++Ln) {
       int64_t v = vstart + 16 * (int64_t)piece_of_lane((uint32_t)Ln);
       P[b][Ln] = (b < nvalid && L != 0 && v + 16 > 0) ? load_piece(q + v) : Piece{{0, 0, 0, 0}};

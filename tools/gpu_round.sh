@@ -38,6 +38,12 @@ for s in $STEPS; do
                python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
                python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive ;;
+    pmcprobe)
+           V=qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl6_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2
+           run pmcprobe1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
+               -d "$OUT/pmcprobe1" -o run --output-format csv -- python3 tools/probe.py --mode ablate --rounds 1 --reps 2 --only $V &&
+           run pmcprobe2 600 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE \
+               -d "$OUT/pmcprobe2" -o run --output-format csv -- python3 tools/probe.py --mode ablate --rounds 1 --reps 2 --only $V ;;
     *) python3 -c "print('unknown step $s')";;
   esac
 done

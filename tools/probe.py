@@ -60,30 +60,33 @@ def ablate_variants(w, a):
     lib = ctypes.CDLL(so)
     lib.probe_rows.restype = ctypes.c_int
     lib.probe_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
-                               ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
+                               ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p]
     out = torch.empty(w.n, dtype=torch.int32, device=w.device)
     blocks = 256
 
-    def mk(qb, pair, nt, abl):
+    def mk(qb, pair, nt, abl, depth):
         def f():
-            rc = lib.probe_rows(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, pair, nt, abl, blocks,
+            rc = lib.probe_rows(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, pair, nt, abl, depth, blocks,
                                 torch.cuda.current_stream().cuda_stream)
-            assert rc == 0, (qb, pair, nt, abl, rc)
+            assert rc == 0, (qb, pair, nt, abl, depth, rc)
         return f
-    combos = [(1, 2, 1, 0), (1, 2, 0, 0), (1, 1, 1, 0), (1, 1, 0, 0), (1, 2, 1, 3), (1, 2, 1, 4), (1, 2, 1, 6),
-              (1, 2, 1, 1), (1, 2, 1, 2), (1, 1, 1, 3), (1, 1, 1, 4), (1, 1, 1, 6)]
+    combos = [(1, 1, 1, 0, 1), (1, 1, 0, 0, 1), (1, 1, 1, 1, 1), (1, 1, 1, 2, 1), (1, 1, 1, 3, 1), (1, 1, 1, 4, 1),
+              (1, 1, 1, 6, 1)]
     if w.L <= 1024:  # aligned uniform bodies: z = 0
-        combos += [(4, 1, 1, 0), (4, 1, 0, 0), (4, 2, 1, 0), (4, 2, 0, 0), (4, 1, 1, 4), (4, 2, 1, 4)]
-    v = {f"qb{qb}_pair{p}_nt{nt}_abl{abl}": (mk(qb, p, nt, abl), w.algo_bytes, None) for qb, p, nt, abl in combos}
+        combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1)]
+    if a.only:
+        keep = set(a.only.split(","))
+        combos = [c for c in combos if "qb{}_pair{}_nt{}_abl{}_d{}".format(*c) in keep]
+    v = {"qb{}_pair{}_nt{}_abl{}_d{}".format(*c): (mk(*c), w.algo_bytes, None) for c in combos}
     # correctness of every non-ablated variant vs the product kernel
     w.step()
     torch.cuda.synchronize()
     ref = w.out.clone()
-    for qb, p, nt, abl in combos:
-        if abl == 0:
-            mk(qb, p, nt, 0)()
+    for c in combos:
+        if c[3] == 0:
+            mk(*c)()
             torch.cuda.synchronize()
-            assert torch.equal(out, ref), (qb, p, nt)
+            assert torch.equal(out, ref), c
     return v
 
 
@@ -94,6 +97,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--grids", default="0,512,1024")
     ap.add_argument("--mode", default="lib", choices=["lib", "ablate"])
+    ap.add_argument("--only", default="", help="comma list of ablate variant names")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     w = Workload(a.config, 0, torch.device("cuda", 0))

@@ -26,22 +26,22 @@ int ensure_tables() {
   return 0;
 }
 
-template <int QB, bool NT, int PAIR, int ABL>
+template <int QB, bool NT, int ABL>
 void go(const ItemsArgs &a, int blocks, hipStream_t s) {
-  constexpr int W = (PAIR == 2 ? 12 : 16);
-  hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, PAIR, ABL, W>), dim3(blocks), dim3(W * 64), 0, s, a);
+  hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, ABL>), dim3(blocks), dim3(1024), 0, s, a);
 }
 } // namespace
 
-#define V(QB, NT, PAIR, ABL)                                                          \
-  if (qb == QB && nt == NT && pair == PAIR && abl == ABL) {                           \
-    go<QB, NT, PAIR, ABL>(a, blocks, s);                                              \
+#define V(QB, NT, ABL)                                                                \
+  if (qb == QB && nt == NT && abl == ABL) {                                           \
+    go<QB, NT, ABL>(a, blocks, s);                                                    \
     return hipGetLastError() == hipSuccess ? 0 : -5;                                  \
   }
 
 extern "C" __attribute__((visibility("default"))) int probe_rows(const uint8_t *d_base, uint64_t n, uint32_t len,
                                                                   uint64_t stride, uint32_t *d_out, int qb, int pair,
-                                                                  int nt, int abl, int blocks, void *stream) {
+                                                                  int nt, int abl, int depth, int blocks,
+                                                                  void *stream) {
   if (ensure_tables()) return -12;
   ItemsArgs a;
   a.base = d_base;
@@ -55,9 +55,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows(const uint8_t *
   a.tq = g_tq;
   a.out = d_out;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  V(1, 1, 2, 0) V(1, 0, 2, 0) V(1, 1, 1, 0) V(1, 0, 1, 0)
-  V(1, 1, 2, 3) V(1, 1, 2, 4) V(1, 1, 2, 6) V(1, 1, 2, 1) V(1, 1, 2, 2)
-  V(1, 1, 1, 3) V(1, 1, 1, 4) V(1, 1, 1, 6)
-  V(4, 1, 1, 0) V(4, 0, 1, 0) V(4, 1, 2, 0) V(4, 0, 2, 0) V(4, 1, 1, 4) V(4, 1, 2, 4)
+  V(1, 1, 0) V(1, 0, 0) V(1, 1, 1) V(1, 1, 2) V(1, 1, 3) V(1, 1, 4) V(1, 1, 6)
+  V(4, 1, 0) V(4, 0, 0) V(4, 1, 3) V(4, 1, 4) V(4, 1, 6)
   return -22;
 }
