@@ -74,7 +74,7 @@ class Workload:
             self.lens_h = from_oracle_free_lengths
             self.offs_h = np.concatenate([[0], np.cumsum(self.lens_h[:-1], dtype=np.uint64)]).astype(np.uint64)
             self.total = int(self.lens_h.sum(dtype=np.uint64))
-            self.base = torch.empty(self.total + 8, dtype=torch.uint8, device=device)
+            self.base = torch.empty((self.total + 15) // 8 * 8, dtype=torch.uint8, device=device)
             self.offs = torch.from_numpy(self.offs_h.view(np.int64)).to(device)
             self.lens = torch.from_numpy(self.lens_h.view(np.int32)).to(device)
             self.meta_bytes = 12 * n
@@ -161,7 +161,7 @@ def cpu_baseline(w: Workload, target_s: float):
     reps = 1
     sm, _ = ref.batch_timed(host, offs, lens, threads=threads, reps=1)
     if sm > 0:
-        reps = max(1, min(200, int(math.ceil(target_s / sm))))
+        reps = max(1, min(5000, int(math.ceil(target_s / sm))))
     sm, _ = ref.batch_timed(host, offs, lens, threads=threads, reps=reps)
     return {
         "value": round(nbytes * reps / sm / GiB, 3),

@@ -244,7 +244,7 @@ struct QuarterInfo {
 // exactly 4 loads and 1 store so the compiler can count vmcnt exactly (the
 // prefetch is never drained early).  Per-task state is plain wave-uniform
 // scalars (SGPRs); item metadata comes from scalar loads.
-template <int QB, bool NT, int ABL = 0>
+template <int QB, bool NT, int ABL = 0, int DEPTH = 1>
 __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
@@ -354,30 +354,78 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t c_len, c_z, c_nr, c_r = 0;
     meta(c_item, c_p0, c_lp, c_len, c_z, c_nr);
     const uint64_t safe = c_p0 & ~(uint64_t)15; // 16-B block holding this wave's first byte
-    u32x4 bufA[4], bufB[4];
-    issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-    auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
-      const bool adv = c_r + 1 < c_nr;
-      const uint64_t n_item = adv ? c_item : c_item + nwaves;
-      const bool ok = n_item < n;
-      uint64_t m_p0, m_lp;
-      uint32_t m_len, m_z, m_nr;
-      meta(ok ? n_item : c_item, m_p0, m_lp, m_len, m_z, m_nr);
-      const uint32_t n_r = adv ? c_r + 1 : 0u;
-      issue(m_p0, m_lp, m_nr, n_r, ok, safe, nb);
-      compute(c_item, c_lp, c_len, c_z, c_nr, c_r, cb);
-      c_item = n_item;
-      c_r = n_r;
-      c_p0 = m_p0;
-      c_lp = m_lp;
-      c_len = m_len;
-      c_z = m_z;
-      c_nr = m_nr;
-      return ok;
+    // Successor of task (item, r) with metadata nr: same item next row, or the
+    // wave's next item.  Invalid successors keep safe (valid) metadata.
+    auto succ = [&](bool ok, uint64_t item, uint32_t r, uint32_t nr, uint64_t &s_item, uint32_t &s_r,
+                    bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr) {
+      const bool adv = r + 1 < nr;
+      s_item = adv ? item : item + nwaves;
+      s_ok = ok && s_item < n;
+      meta(s_ok ? s_item : c_item, p0, lp, len, z, snr);
+      s_r = adv ? r + 1 : 0u;
     };
-    for (;;) {
-      if (!step(bufA, bufB)) break;
-      if (!step(bufB, bufA)) break;
+    if constexpr (DEPTH == 1) {
+      u32x4 bufA[4], bufB[4];
+      issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
+        uint64_t m_item, m_p0, m_lp;
+        uint32_t m_r, m_len, m_z, m_nr;
+        bool ok;
+        succ(true, c_item, c_r, c_nr, m_item, m_r, ok, m_p0, m_lp, m_len, m_z, m_nr);
+        issue(m_p0, m_lp, m_nr, m_r, ok, safe, nb);
+        compute(c_item, c_lp, c_len, c_z, c_nr, c_r, cb);
+        c_item = m_item;
+        c_r = m_r;
+        c_p0 = m_p0;
+        c_lp = m_lp;
+        c_len = m_len;
+        c_z = m_z;
+        c_nr = m_nr;
+        return ok;
+      };
+      for (;;) {
+        if (!step(bufA, bufB)) break;
+        if (!step(bufB, bufA)) break;
+      }
+    } else {
+      // DEPTH = 2: the next two rows' loads are in flight while one computes.
+      u32x4 bufA[4], bufB[4], bufC[4];
+      uint64_t n_item, n_p0, n_lp;
+      uint32_t n_r, n_len, n_z, n_nr;
+      bool n_ok;
+      issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
+      succ(true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_p0, n_lp, n_len, n_z, n_nr);
+      issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
+      bool c_ok = true;
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
+        uint64_t m_item, m_p0, m_lp;
+        uint32_t m_r, m_len, m_z, m_nr;
+        bool m_ok;
+        succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr);
+        issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
+        compute(c_item, c_lp, c_len, c_z, c_nr, c_r, cb);
+        c_ok = n_ok;
+        c_item = n_item;
+        c_r = n_r;
+        c_lp = n_lp;
+        c_len = n_len;
+        c_z = n_z;
+        c_nr = n_nr;
+        n_ok = m_ok;
+        n_item = m_item;
+        n_r = m_r;
+        n_p0 = m_p0;
+        n_lp = m_lp;
+        n_len = m_len;
+        n_z = m_z;
+        n_nr = m_nr;
+        return c_ok;
+      };
+      for (;;) {
+        if (!step(bufA, bufC)) break;
+        if (!step(bufB, bufA)) break;
+        if (!step(bufC, bufB)) break;
+      }
     }
     flush();
   } else {
@@ -447,19 +495,41 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint64_t g = gw;
     if (g >= ngroups) return;
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
-    u32x4 bufA[4], bufB[4];
-    issue(g, true, safe, bufA);
-    auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
-      const uint64_t ng = g + nwaves;
-      const bool ok = ng < ngroups;
-      issue(ok ? ng : g, ok, safe, nb);
-      compute(g, cb);
-      g = ng;
-      return ok;
-    };
-    for (;;) {
-      if (!step(bufA, bufB)) break;
-      if (!step(bufB, bufA)) break;
+    if constexpr (DEPTH == 1) {
+      u32x4 bufA[4], bufB[4];
+      issue(g, true, safe, bufA);
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
+        const uint64_t ng = g + nwaves;
+        const bool ok = ng < ngroups;
+        issue(ok ? ng : g, ok, safe, nb);
+        compute(g, cb);
+        g = ng;
+        return ok;
+      };
+      for (;;) {
+        if (!step(bufA, bufB)) break;
+        if (!step(bufB, bufA)) break;
+      }
+    } else {
+      u32x4 bufA[4], bufB[4], bufC[4];
+      issue(g, true, safe, bufA);
+      {
+        const uint64_t g1 = g + nwaves;
+        issue(g1 < ngroups ? g1 : g, g1 < ngroups, safe, bufB);
+      }
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
+        const uint64_t g2 = g + 2 * nwaves;
+        const bool ok2 = g2 < ngroups;
+        issue(ok2 ? g2 : g, ok2, safe, fb);
+        compute(g, cb);
+        g += nwaves;
+        return g < ngroups;
+      };
+      for (;;) {
+        if (!step(bufA, bufC)) break;
+        if (!step(bufB, bufA)) break;
+        if (!step(bufC, bufB)) break;
+      }
     }
     flush();
   }

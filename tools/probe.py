@@ -71,9 +71,10 @@ def ablate_variants(w, a):
             assert rc == 0, (qb, pair, nt, abl, depth, rc)
         return f
     combos = [(1, 1, 1, 0, 1), (1, 1, 0, 0, 1), (1, 1, 1, 1, 1), (1, 1, 1, 2, 1), (1, 1, 1, 3, 1), (1, 1, 1, 4, 1),
-              (1, 1, 1, 6, 1)]
+              (1, 1, 1, 6, 1), (1, 1, 1, 0, 2), (1, 1, 0, 0, 2), (1, 1, 1, 3, 2)]
     if w.L <= 1024:  # aligned uniform bodies: z = 0
-        combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1)]
+        combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
+                   (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)]
     if a.only:
         keep = set(a.only.split(","))
         combos = [c for c in combos if "qb{}_pair{}_nt{}_abl{}_d{}".format(*c) in keep]

@@ -26,15 +26,15 @@ int ensure_tables() {
   return 0;
 }
 
-template <int QB, bool NT, int ABL>
+template <int QB, bool NT, int ABL, int DEPTH>
 void go(const ItemsArgs &a, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, ABL>), dim3(blocks), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, ABL, DEPTH>), dim3(blocks), dim3(1024), 0, s, a);
 }
 } // namespace
 
-#define V(QB, NT, ABL)                                                                \
-  if (qb == QB && nt == NT && abl == ABL) {                                           \
-    go<QB, NT, ABL>(a, blocks, s);                                                    \
+#define V(QB, NT, ABL, D)                                                             \
+  if (qb == QB && nt == NT && abl == ABL && depth == D) {                             \
+    go<QB, NT, ABL, D>(a, blocks, s);                                                 \
     return hipGetLastError() == hipSuccess ? 0 : -5;                                  \
   }
 
@@ -55,7 +55,8 @@ extern "C" __attribute__((visibility("default"))) int probe_rows(const uint8_t *
   a.tq = g_tq;
   a.out = d_out;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  V(1, 1, 0) V(1, 0, 0) V(1, 1, 1) V(1, 1, 2) V(1, 1, 3) V(1, 1, 4) V(1, 1, 6)
-  V(4, 1, 0) V(4, 0, 0) V(4, 1, 3) V(4, 1, 4) V(4, 1, 6)
+  V(1, 1, 0, 1) V(1, 0, 0, 1) V(1, 1, 1, 1) V(1, 1, 2, 1) V(1, 1, 3, 1) V(1, 1, 4, 1) V(1, 1, 6, 1)
+  V(1, 1, 0, 2) V(1, 0, 0, 2) V(1, 1, 3, 2)
+  V(4, 1, 0, 1) V(4, 0, 0, 1) V(4, 1, 3, 1) V(4, 1, 4, 1) V(4, 1, 6, 1) V(4, 1, 0, 2) V(4, 1, 3, 2)
   return -22;
 }
