@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
+    p.add_argument("--prewarm-s", type=float, default=0.5,
+                   help="untimed steps before the W warmup steps until this much time has passed: the GPU "
+                        "clock ramps over the first ~20 launches of sustained load (DESIGN.md 5)")
     return p.parse_args()
 
 
@@ -196,19 +199,21 @@ def host_inclusive(w: Workload):
 
 
 def stream_read_probe(w: Workload, reps=10):
-    """Achievable HBM read rate on the same buffer (coalesced 16-B lanes)."""
+    """Achievable HBM read rate on the same buffer: a pure streaming read with
+    coalesced 16-B lanes, non-temporal (the CRC kernel's load shape) and
+    temporal.  The rows kernel's ceiling is the nt1 number, not 8 TB/s."""
     nbytes = (w.total // 4096) * 4096
     stream = torch.cuda.current_stream()
     res = {}
-    for pattern in (0, 1):
-        rpc_amd.stream_read(w.base, pattern, nbytes=nbytes)
+    for nt in (1, 0):
+        rpc_amd.stream_read(w.base, 0, nontemporal=bool(nt), nbytes=nbytes)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(reps):
-            rpc_amd.stream_read(w.base, pattern, nbytes=nbytes)
+            rpc_amd.stream_read(w.base, 0, nontemporal=bool(nt), nbytes=nbytes)
         e1.record(stream)
         e1.synchronize()
-        res[f"pattern{pattern}_GBps"] = round(nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+        res[f"coalesced_nt{nt}_GBps"] = round(nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
     return res
 
 
@@ -243,6 +248,12 @@ def main():
 
     w = Workload(args.config, rank, device)
     stream = torch.cuda.current_stream()
+    prewarm_steps = 0
+    t_pw = time.perf_counter()
+    while time.perf_counter() - t_pw < args.prewarm_s:
+        w.step()
+        torch.cuda.synchronize()
+        prewarm_steps += 1
     for _ in range(args.warmup):
         w.step()
     torch.cuda.synchronize()
@@ -303,11 +314,12 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / (HBM_PEAK_BPS / 1e9), 4),
                 "traffic": traffic,
-                "kernel": "crc32_items_kernel" if w.kind != "large" else "crc32_items_kernel (+combine)",
+                "kernel": "crc32_rows_kernel" if w.kind != "large" else "crc32_rows_kernel (+chunk combine)",
                 "avg_launch_us": round(kernel_s * 1e6, 2),
                 "algo_bytes_per_launch": w.algo_bytes,
             },
             "cpu_baseline": cpu,
+            "prewarm": {"seconds": args.prewarm_s, "steps": prewarm_steps},
             "device": rpc_amd.device_info(),
             "extra": extra,
         }

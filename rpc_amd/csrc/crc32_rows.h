@@ -202,6 +202,8 @@ __device__ __forceinline__ uint32_t seed_for(const uint8_t *lds, uint32_t first)
 constexpr int kRowsAblNoCompute = 1; // XOR fold instead of the slice-by-4 chain
 constexpr int kRowsAblNoMerge = 2;   // skip the per-lane shift / reductions
 constexpr int kRowsAblNoLoad = 4;    // synthesize row data instead of loading it
+constexpr int kRowsAblNaturalOrder = 8; // lane L loads piece L (timing only: wrong CRCs)
+constexpr int kRowsAblNoStore = 16;     // results never stored (timing / codegen only)
 
 namespace rows {
 
@@ -251,7 +253,20 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   {
     const uint4 *src = a.lds_image;
     uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
-    for (uint32_t k = threadIdx.x; k < kLdsBytesV2 / 16; k += blockDim.x) dst[k] = src[k];
+    // All of this thread's image loads in flight at once (a rolled loop would
+    // pay one L2 round trip per 16 KiB before the first HBM byte is read).
+    constexpr uint32_t kImg16 = kLdsBytesV2 / 16, kPer = (kImg16 + 1023) / 1024;
+    uint4 t[kPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+      const uint32_t k = threadIdx.x + i * 1024u;
+      if (k < kImg16) t[i] = src[k];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+      const uint32_t k = threadIdx.x + i * 1024u;
+      if (k < kImg16) dst[k] = t[i];
+    }
   }
   __syncthreads();
   const uint8_t *lds = reinterpret_cast<const uint8_t *>(s_lds);
@@ -260,14 +275,27 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   const uint32_t lane4 = (lane & 31u) * 4u;
   const uint32_t lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);
   const uint32_t hi = lane >> 4;                   // 16-lane row = quarter after the transpose
-  const uint32_t pofs = 16u * piece_of_lane(lane); // byte offset of this lane's piece in a quarter
+  // byte offset of this lane's piece in a quarter
+  const uint32_t pofs = 16u * (((ABL & kRowsAblNaturalOrder) != 0) ? lane : piece_of_lane(lane));
   const uint32_t st1_base = kLdsST1 + lane4;
   const uint32_t st2_base = kLdsST2 + hi * 4u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * 16u;
-  const uint64_t gw = (uint64_t)blockIdx.x * 16u + wave;
+  // Tasks (QB = 1: items, QB = 4: groups of 4 items) are dealt round-robin:
+  // wave gw takes gw, gw + nwaves, ...  All waves then stream one contiguous
+  // window of HBM (blocked ranges put 4096 streams 1 MiB apart in lockstep:
+  // measured 6 % slower).  gw is XCD-aware: workgroups are dispatched round-
+  // robin over the 8 XCDs, so virtual block vb = (b % 8) * (blocks / 8) + b / 8
+  // makes the 32 waves whose CRCs share a 128-B output line live on one XCD,
+  // whose L2 assembles the whole line (measured: strided 4-B stores from two
+  // XCDs per line cost 3.5 % of the kernel).
+  const uint32_t nblk = gridDim.x;
+  const uint32_t vb = (nblk % 8u == 0u) ? (blockIdx.x % 8u) * (nblk / 8u) + blockIdx.x / 8u : blockIdx.x;
+  const uint64_t gw = (uint64_t)vb * 16u + wave;
   const uint32_t mode = a.mode;
   const uint64_t n = a.n_items;
+  const uint64_t n_tasks = (QB == 4) ? (n + 3) / 4 : n;
+  if (gw >= n_tasks) return;
 
   auto synth = [&](uint64_t key, u32x4 (&buf)[4]) {
 #pragma unroll
@@ -315,8 +343,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // store would make the compiler drain vmcnt (store-data WAR) every row.
     uint32_t outv = 0, ocount = 0;
     uint64_t j0 = 0;
+    uint32_t sink = 0;
     auto flush = [&]() {
-      if (lane < ocount) a.out[gw + (j0 + lane) * nwaves] = outv;
+      if constexpr ((ABL & kRowsAblNoStore) == 0) {
+        if (lane < ocount) a.out[gw + (j0 + lane) * nwaves] = outv;
+      } else {
+        sink ^= outv;
+      }
       j0 += ocount;
       ocount = 0;
     };
@@ -324,7 +357,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       outv = (lane == ocount) ? res : outv;
       if (++ocount == 64u) flush();
     };
-    auto compute = [&](uint64_t item, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r,
+    auto compute = [&](bool valid, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r,
                        u32x4 (&buf)[4]) {
       const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
       const bool last = r + 1 == nr;
@@ -344,36 +377,44 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         uint32_t res = W;
         if (z != 0) res = nib_map<64u, 2u>(lds, res, kLdsZI2 + (z - 1u) * 512u);
         if (mode == kModeFinal) res = ~res;
-        park(res);
+        if (valid) park(res);
       }
     };
 
     uint64_t c_item = gw;
-    if (c_item >= n) return;
     uint64_t c_p0, c_lp;
     uint32_t c_len, c_z, c_nr, c_r = 0;
     meta(c_item, c_p0, c_lp, c_len, c_z, c_nr);
     const uint64_t safe = c_p0 & ~(uint64_t)15; // 16-B block holding this wave's first byte
     // Successor of task (item, r) with metadata nr: same item next row, or the
-    // wave's next item.  Invalid successors keep safe (valid) metadata.
+    // wave's next item.  Invalid successors carry the wave's first item's
+    // (in-range) metadata and load from `safe`; their results are dropped.
     auto succ = [&](bool ok, uint64_t item, uint32_t r, uint32_t nr, uint64_t &s_item, uint32_t &s_r,
                     bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr) {
       const bool adv = r + 1 < nr;
       s_item = adv ? item : item + nwaves;
       s_ok = ok && s_item < n;
-      meta(s_ok ? s_item : c_item, p0, lp, len, z, snr);
+      meta(s_ok ? s_item : gw, p0, lp, len, z, snr);
       s_r = adv ? r + 1 : 0u;
     };
+    // The unrolled loops have ONE exit, at the bottom: a mid-body break edge
+    // (structurized back through the loop header) would carry the first
+    // half's in-flight prefetch into the header, and the compiler would then
+    // drain vmcnt before every prefetch (measured: rows fully serialised on
+    // half the iterations).  Trailing steps past the wave's last task run on
+    // invalid tasks (c_ok false): safe loads, no result parked.
+    bool c_ok = true;
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
         uint64_t m_item, m_p0, m_lp;
         uint32_t m_r, m_len, m_z, m_nr;
-        bool ok;
-        succ(true, c_item, c_r, c_nr, m_item, m_r, ok, m_p0, m_lp, m_len, m_z, m_nr);
-        issue(m_p0, m_lp, m_nr, m_r, ok, safe, nb);
-        compute(c_item, c_lp, c_len, c_z, c_nr, c_r, cb);
+        bool m_ok;
+        succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr);
+        issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, cb);
+        c_ok = m_ok;
         c_item = m_item;
         c_r = m_r;
         c_p0 = m_p0;
@@ -381,12 +422,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         c_len = m_len;
         c_z = m_z;
         c_nr = m_nr;
-        return ok;
       };
-      for (;;) {
-        if (!step(bufA, bufB)) break;
-        if (!step(bufB, bufA)) break;
-      }
+      do {
+        step(bufA, bufB);
+        step(bufB, bufA);
+      } while (c_ok);
     } else {
       // DEPTH = 2: the next two rows' loads are in flight while one computes.
       u32x4 bufA[4], bufB[4], bufC[4];
@@ -396,14 +436,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
       succ(true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_p0, n_lp, n_len, n_z, n_nr);
       issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
-      bool c_ok = true;
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) {
         uint64_t m_item, m_p0, m_lp;
         uint32_t m_r, m_len, m_z, m_nr;
         bool m_ok;
         succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
-        compute(c_item, c_lp, c_len, c_z, c_nr, c_r, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, cb);
         c_ok = n_ok;
         c_item = n_item;
         c_r = n_r;
@@ -419,15 +458,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         n_len = m_len;
         n_z = m_z;
         n_nr = m_nr;
-        return c_ok;
       };
-      for (;;) {
-        if (!step(bufA, bufC)) break;
-        if (!step(bufB, bufA)) break;
-        if (!step(bufC, bufB)) break;
-      }
+      do {
+        step(bufA, bufC);
+        step(bufB, bufA);
+        step(bufC, bufB);
+      } while (c_ok);
     }
     flush();
+    if constexpr ((ABL & kRowsAblNoStore) != 0)
+      if (sink == 0x9E3779B9u) a.out[gw] = sink; // keeps the results live
   } else {
     // QB = 4: group g = items [4g, 4g+4), quarter b <-> item 4g+b (len + pad <= 1 KiB).
     const uint64_t ngroups = (n + 3) / 4;
@@ -457,7 +497,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         }
       }
     };
-    // Parked results: lane k = item 4*(gw + (j0 + k/4) * nwaves) + k%4 (see QB = 1).
+    // Parked results: lane k = item 4 * (gw + (j0 + k / 4) * nwaves) + k % 4 (see QB = 1).
     uint32_t outv = 0, ocount = 0;
     uint64_t j0 = 0;
     auto flush = [&]() {
@@ -493,7 +533,6 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       if (ocount == 64u) flush();
     };
     uint64_t g = gw;
-    if (g >= ngroups) return;
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];

@@ -27,6 +27,8 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py ;;
     probe) run probe 600 python tools/probe.py ;;
     ablate) run ablate 600 python tools/probe.py --mode ablate --rounds 3 ;;
+    ablate_nat) run ablate_nat 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2,qb1_pair1_nt1_abl3_d2,qb1_pair1_nt1_abl16_d1 ;;
+    sustain) run sustain 600 python tools/probe.py --mode sustain --launches 60 --only product,stream_nt1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2 ;;
     ablate_c1) run ablate_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 ;;
     bench_c1) run bench_c1 600 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive ;;
     bench_c2) run bench_c2 600 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive ;;
@@ -35,9 +37,9 @@ for s in $STEPS; do
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive &&
+               python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-inclusive ;;
+               python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive ;;
     pmcprobe)
            V=qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl6_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2
            run pmcprobe1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \

@@ -4,6 +4,9 @@
 
   python tools/probe.py [--config ns] [--rounds 5] [--reps 10] [--mode lib|ablate]
 mode lib:    stream-read patterns and the product kernel under its runtime options.
+mode sustain: each --only variant (ablate names, "product", "stream_nt1")
+             launched --launches times back to back with per-launch events,
+             while a child process samples power/clocks (DVFS under load).
 mode ablate: tools/libprobe.so variants (ABL bits: 1 no-compute, 2 no-combine,
              4 no-load; DEPTH rows in flight; NT loads).  Ablated outputs are
              wrong by construction -- timing only; abl=0 outputs are checked
@@ -53,7 +56,7 @@ def lib_variants(w, a):
 
 def ablate_variants(w, a):
     """Rows-kernel variants: (qb, pair, nt, abl) -- abl bits 1 no-compute,
-    2 no-merge, 4 no-load."""
+    2 no-merge, 4 no-load, 8 natural lane->piece load order."""
     so = os.path.join(REPO, "tools", "libprobe.so")
     if not os.path.exists(so):
         subprocess.run(["make", "-C", os.path.join(REPO, "tools")], check=True)
@@ -71,7 +74,9 @@ def ablate_variants(w, a):
             assert rc == 0, (qb, pair, nt, abl, depth, rc)
         return f
     combos = [(1, 1, 1, 0, 1), (1, 1, 0, 0, 1), (1, 1, 1, 1, 1), (1, 1, 1, 2, 1), (1, 1, 1, 3, 1), (1, 1, 1, 4, 1),
-              (1, 1, 1, 6, 1), (1, 1, 1, 0, 2), (1, 1, 0, 0, 2), (1, 1, 1, 3, 2)]
+              (1, 1, 1, 6, 1), (1, 1, 1, 0, 2), (1, 1, 0, 0, 2), (1, 1, 1, 3, 2),
+              (1, 1, 1, 8, 1), (1, 1, 1, 11, 1), (1, 1, 1, 9, 1), (1, 1, 0, 11, 1), (1, 1, 0, 3, 1),
+              (1, 1, 1, 16, 1), (1, 1, 1, 19, 1)]
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
                    (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)]
@@ -91,17 +96,89 @@ def ablate_variants(w, a):
     return v
 
 
+def sample_smi(stop, log):
+    """Child-process power/clock sampler (best effort; rocm-smi or amd-smi)."""
+    import threading  # noqa: F401
+    import time
+    cmds = [["amd-smi", "metric", "-g", "0", "-p", "-c"], ["rocm-smi", "-d", "0", "--showpower", "--showclocks"]]
+    cmd = None
+    for c in cmds:
+        try:
+            r = subprocess.run(c, capture_output=True, text=True, timeout=10)
+            if r.returncode == 0:
+                cmd = c
+                break
+        except (OSError, subprocess.SubprocessError):
+            pass
+    if cmd is None:
+        return
+    t0 = time.perf_counter()
+    while not stop.is_set():
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=10)
+            log.append((round(time.perf_counter() - t0, 3), r.stdout))
+        except (OSError, subprocess.SubprocessError):
+            break
+        time.sleep(0.05)
+
+
+def sustain(w, a):
+    import threading
+    import time
+    names = a.only.split(",") if a.only else ["product", "stream_nt1"]
+    abl = ablate_variants(w, argparse.Namespace(only=",".join(n for n in names if n.startswith("qb"))))
+    nbytes = (w.total // 4096) * 4096
+    fns = {}
+    for n in names:
+        if n == "product":
+            fns[n] = (w.step, w.algo_bytes)
+        elif n == "stream_nt1":
+            fns[n] = (lambda: rpc_amd.stream_read(w.base, 0, True, nbytes=nbytes), nbytes)
+        else:
+            fns[n] = (abl[n][0], abl[n][1])
+    s = torch.cuda.current_stream()
+    smi_log = []
+    stop = threading.Event()
+    th = threading.Thread(target=sample_smi, args=(stop, smi_log), daemon=True)
+    th.start()
+    t0 = time.perf_counter()
+    for n, (fn, nb) in fns.items():
+        time.sleep(2.0)  # let the clocks recover between variants
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.launches + 1)]
+        tstart = time.perf_counter() - t0
+        ev[0].record(s)
+        for i in range(a.launches):
+            fn()
+            ev[i + 1].record(s)
+        ev[-1].synchronize()
+        d = [ev[i].elapsed_time(ev[i + 1]) * 1e3 for i in range(a.launches)]
+        q = len(d) // 4
+        print(json.dumps({"variant": n, "config": a.config, "t_start_s": round(tstart, 2),
+                          "first10_us": round(statistics.mean(d[:10]), 1),
+                          "last_quarter_us": round(statistics.mean(d[-q:]), 1),
+                          "min_us": round(min(d), 1), "max_us": round(max(d), 1),
+                          "mean_GBps": round(nb / (statistics.mean(d) / 1e6) / 1e9, 1),
+                          "per_launch_us": [round(x, 1) for x in d]}), flush=True)
+    stop.set()
+    th.join(timeout=15)
+    for t, out in smi_log:
+        print(json.dumps({"smi_t_s": t, "out": out.strip()[-600:]}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="ns")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--grids", default="0,512,1024")
-    ap.add_argument("--mode", default="lib", choices=["lib", "ablate"])
+    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain"])
+    ap.add_argument("--launches", type=int, default=60)
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     w = Workload(a.config, 0, torch.device("cuda", 0))
+    if a.mode == "sustain":
+        return sustain(w, a)
     variants = lib_variants(w, a) if a.mode == "lib" else ablate_variants(w, a)
     res = {k: [] for k in variants}
     for _ in range(a.rounds):
