@@ -1,26 +1,18 @@
 // rpc_amd/csrc/crc32_kernels.hip -- batched CRC-32 (zlib / ISO-HDLC) for gfx950.
 //
 // Replaces the arithmetic behind rpc_crc32() (reference crc.c:4-9 -> zlib crc32)
-// with a many-buffer device path.  Design:
+// with a many-buffer device path:
 //
-//  * Persistent grid, one 1024-thread workgroup (16 waves) per CU.  Each
-//    workgroup copies the 156 KiB table image (crc32_layout.h) into LDS once.
-//  * An "item" (one body, or one chunk of a large body) is owned by a group of
-//    G lanes (G = 64: one wavefront per body; G = 16: four bodies per wave).
-//  * Items are cut into ROWS of G*64 bytes aligned to the END of the item; lane
-//    j of the group CRCs the 64-byte segment [row + 64j, row + 64j + 64) with
-//    slice-by-4 lookups (one v_perm_b32 forms each LDS address, all lookups
-//    bank-conflict-free thanks to 32 bank-replicated copies).
-//  * Lane partials are merged by a per-lane GF(2) shift A_{64(G-1-j)} done as
-//    two conflict-free nibble-table steps plus wavefront XOR shuffles, giving
-//    crc0(row).  Rows are folded by Horner: W = A_ROW(W) ^ crc0(row).
-//  * The zlib 0xFFFFFFFF pre-conditioning enters as W0 = A_q(0xFFFFFFFF) with q
-//    the byte count of the first (partial) row (table Tq), so no per-body
-//    exponentiation is needed.  Bodies whose end is not 16-byte aligned are
-//    treated as body||0^z with z = pad to 16, loads stay 16-byte aligned, and the
-//    z zero bytes are removed at the end with A_z^-1 (table ZI).
-//  * Loads are 16 B per lane (global_load_dwordx4), software-pipelined one row
-//    ahead across items.  No MFMA: this is a byte scan.
+//  * crc32_rows_kernel (crc32_rows.h): persistent grid, one 1024-thread
+//    workgroup (16 waves) per CU with the 155 KiB table image in LDS; a wave
+//    CRCs one 4 KiB row per step (QB = 1: rows of one body, end-aligned, Horner
+//    across rows; QB = 4: four <= 1 KiB bodies per row).  Coalesced 16-B
+//    non-temporal loads, permlane transpose, slice-by-4 lookups, GF(2) merge.
+//  * crc32_chunk_combine_kernel (below): folds chunk CRCs of large bodies
+//    (zlib crc32_combine algebra), one wave per body.
+//  * splitmix_fill_kernel / stream_read_kernel: synthetic data and the
+//    achievable-HBM-read probe used by bench.py.
+//  No MFMA: this is a byte scan.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

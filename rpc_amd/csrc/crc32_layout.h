@@ -38,7 +38,10 @@ constexpr uint32_t kTqEntries = kMaxRow + 1; // Tq[q] = A_q(0xFFFFFFFF), q=0..40
 constexpr uint32_t row_bytes(int G) { return (uint32_t)G * kSegBytes; }
 
 // ---- rows-kernel image (crc32_rows.h): main tables as above, then
-//   ST1 16 KiB  ST1[n][nib][c]  = A_{64*(15-(c&15))}(nib << 4n), c = lane & 31
+//   ST1 16 KiB  A_{64*(15-(c&15))}(nib << 4n), c = lane & 31, at
+//               ST1 + (n/2)*4096 + nib*256 + (n%2)*128 + c*4: one v_perm_b32 of
+//               the masked nibble vector forms the address (like MAIN), the
+//               n/2 part rides in the ds_read immediate offset
 //   ST2  2 KiB  ST2[n][nib][hi] = A_{1024*(3-hi)}(nib << 4n),    hi = 0..3
 //   RW  512 B   RW[n][nib]      = A_4096(nib << 4n)
 //   ZI  7.5 KiB ZI[z-1][n][nib] = A_z^-1(nib << 4n)
@@ -50,6 +53,8 @@ constexpr uint32_t kLdsZI2 = kLdsRW2 + 512;   // 150016
 // TQ16[k] = A_{16k}(0xFFFFFFFF), k = 0..256: zlib pre-conditioning seeds for
 // first rows of 16k bytes (other lengths: round up, undo with ZI).
 constexpr uint32_t kLdsTQ16 = kLdsZI2 + 15 * 512; // 157696
+// A zero dword (TQ16's 12-byte tail pad): lanes with nothing to look up read it.
+constexpr uint32_t kLdsZero = kLdsTQ16 + 1028;
 static_assert(kLdsTQ16 + 1040 == kLdsBytesV2, "rows image size");
 static_assert(kLdsBytesV2 % 16 == 0 && kLdsBytesV2 <= 163840, "fits the 160 KiB LDS");
 void build_lds_image_v2(uint32_t *img /* kLdsBytesV2 bytes */);

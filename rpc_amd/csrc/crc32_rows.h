@@ -14,10 +14,16 @@
 //              v_bitop3_b32 (3-way XOR) fold the lookups and the next dword.
 //   merge:     crc0(row) = XOR_L' A_{64*(63-L')} c_L'
 //                        = XOR_hi A_{1024*(3-hi)} XOR_lo A_{64*(15-lo)} c_{hi,lo},
-//              hi = L' >> 4 (the quarter), lo = L' & 15: nibble step ST1
-//              (per lane), DPP quad + row_ror reduction over lo, nibble step
-//              ST2 (per row), permlane16/32-swap reductions over hi.  All
-//              reductions are VALU; no LDS traffic besides the 16 nibble reads.
+//              hi = L' >> 4 (the quarter), lo = L' & 15.  Step 1 (per lane):
+//              ST1 shift, 8 lookups each formed by ONE v_perm_b32 from the
+//              even/odd nibble vectors; DPP quad + row_ror XOR over lo.
+//              Step 2 (values now uniform per 16-lane row): "distributed" --
+//              lane lo < 8 looks up nibble lo of its row's value in ST2, and in
+//              the same ds_read lanes 8..15 of row 0 look up the nibbles of the
+//              running item CRC W in RW (Horner A_4096); DPP + permlane-swap
+//              reductions, readlane 4 / 12 -> crc0(row), A_4096(W) as SGPRs.
+//              Seeds A_first(0xFFFFFFFF) are scalar loads from the global Tq
+//              table; the trailing-pad undo ZI is another distributed step.
 // QB = 1: the row is 4 KiB of one item (items of any length, end-aligned rows,
 //         Horner across rows with RW, Tq pre-conditioning, ZI trailing-pad undo).
 // QB = 4: the row holds four items of <= 1 KiB each (item = quarter = hi), so
@@ -25,7 +31,7 @@
 //
 // LDS image (crc32_layout.h "v3"):
 //   MAIN [0,128K)  slice-by-4 tables x32 copies (two tables per 256-B row)
-//   ST1  16 KiB    ST1[n][nib][c]  = A_{64*(15-(c&15))}(nib<<4n), c = lane&31
+//   ST1  16 KiB    A_{64*(15-(c&15))}(nib<<4n), c = lane&31, perm-addressable
 //   ST2  2 KiB     ST2[n][nib][hi] = A_{1024*(3-hi)}(nib<<4n)
 //   RW   512 B     RW[n][nib]      = A_4096(nib<<4n)
 //   ZI   7.5 KiB   ZI[z-1][n][nib] = A_z^-1(nib<<4n)
@@ -68,13 +74,6 @@ __device__ __forceinline__ uint32_t slice4w(const uint8_t *lds, uint32_t x, uint
   return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(t3, t2, t1, 0x96), t0, w, 0x96);
 }
 
-template <uint32_t STRIDE, uint32_t SHIFT>
-__device__ __forceinline__ uint32_t nib_map(const uint8_t *lds, uint32_t s, uint32_t base) {
-  uint32_t r = 0;
-#pragma unroll
-  for (uint32_t n = 0; n < 8; ++n) r ^= lds_ld(lds, base + n * STRIDE + (((s >> (4 * n)) & 15u) << SHIFT));
-  return r;
-}
 
 // DPP lane moves (all lanes active, every source valid).
 __device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) { // quad_perm [1,0,3,2]
@@ -88,6 +87,9 @@ __device__ __forceinline__ uint32_t dpp_ror4(uint32_t v) { // row_ror:4
 }
 __device__ __forceinline__ uint32_t dpp_ror8(uint32_t v) { // row_ror:8
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_shr4(uint32_t v) { // row_shr:4, zeros shifted in
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t swz_xor16(uint32_t v) { // ds_swizzle bit mode, xor 16
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
@@ -186,14 +188,57 @@ __device__ __forceinline__ T ld_const(const T *p, uint64_t i) {
   return ((const __attribute__((address_space(4))) T *)(p))[i];
 }
 
-// A_first(0xFFFFFFFF), the zlib pre-conditioning seed for a first row of
-// `first` bytes: TQ16 holds multiples of 16; other lengths round up and undo
-// the extra bytes with the ZI inverse-shift tables.
-__device__ __forceinline__ uint32_t seed_for(const uint8_t *lds, uint32_t first) {
-  const uint32_t up = (first + 15u) & ~15u;
-  uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
-  if (up != first) w = nib_map<64u, 2u>(lds, w, kLdsZI2 + (up - first - 1u) * 512u);
-  return w;
+// Per-lane ST1 step A_{64*(15-lo)}(s): the nibbles of s are split into two
+// byte vectors (even / odd nibbles) so that ONE v_perm_b32 per lookup forms
+// the address {copy | (nibble << 8) | (2 << 16)} exactly like the main tables
+// (ST1 sits at 2 << 16); the nibble pair index rides in the immediate offset.
+__device__ __forceinline__ uint32_t st1_map(const uint8_t *lds, uint32_t s, uint32_t lsel1) {
+  const uint32_t xl = s & 0x0F0F0F0Fu, xh = (s >> 4) & 0x0F0F0F0Fu;
+  uint32_t t[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    t[2 * k] = lds_ld(lds, __builtin_amdgcn_perm(xl, lsel1, 0x0C020400u + (k << 8)) + k * 4096u);
+    t[2 * k + 1] = lds_ld(lds, __builtin_amdgcn_perm(xh, lsel1, 0x0C020401u + (k << 8)) + k * 4096u);
+  }
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// "Distributed" nibble steps for values that are uniform over a 16-lane row
+// (or the whole wave): lane n = lane & 7 of the row looks up nibble n only, one
+// ds_read per lane instead of eight, and a 3-step DPP XOR (quad xor1, xor2,
+// row_shr 4) leaves the 8-lane sums in lanes 4..7 (and 12..15) of each row.
+__device__ __forceinline__ uint32_t dist_reduce8(uint32_t t) {
+  t ^= dpp_xor1(t);
+  t ^= dpp_xor2(t);
+  return t ^ dpp_shr4(t);
+}
+
+// Per-lane constants of the distributed steps (computed once per kernel).
+struct DistLane {
+  uint32_t shift;  // 4 * (lane & 7): which nibble this lane looks up
+  uint32_t n64;    // (lane & 7) * 64: nibble-table row ([n][nib] tables, 64 B per n)
+  uint32_t row_base; // merge step: lo < 8 -> ST2 + lo*256 + hi*4; hi == 0, lo >= 8 -> RW2 + (lo-8)*64; else kLdsZero
+  uint32_t row_mul;  // merge step: nibble stride (16 for ST2, 4 for RW2, 0 for the zero lanes)
+  bool own;          // merge step: lane looks up its own row's value (lo < 8)
+};
+
+__device__ __forceinline__ DistLane dist_lane(uint32_t lane) {
+  DistLane d;
+  const uint32_t lo = lane & 15u, hi = lane >> 4;
+  d.shift = 4u * (lane & 7u);
+  d.n64 = (lane & 7u) * 64u;
+  d.own = lo < 8u;
+  d.row_base = d.own ? kLdsST2 + lo * 256u + hi * 4u : (hi == 0u ? kLdsRW2 + (lo - 8u) * 64u : kLdsZero);
+  d.row_mul = d.own ? 16u : (hi == 0u ? 4u : 0u);
+  return d;
+}
+
+// Nibble map of a wave-uniform value u by a [n][nib] table at `table`
+// (RW2 / ZI2 layout); result is wave-uniform (read from lane 4).
+__device__ __forceinline__ uint32_t dist_uniform(const uint8_t *lds, uint32_t u, uint32_t table, const DistLane &d) {
+  const uint32_t nib = (u >> d.shift) & 15u;
+  const uint32_t t = dist_reduce8(lds_ld(lds, table + d.n64 + nib * 4u));
+  return (uint32_t)__builtin_amdgcn_readlane((int)t, 4);
 }
 
 } // namespace rows
@@ -204,6 +249,9 @@ constexpr int kRowsAblNoMerge = 2;   // skip the per-lane shift / reductions
 constexpr int kRowsAblNoLoad = 4;    // synthesize row data instead of loading it
 constexpr int kRowsAblNaturalOrder = 8; // lane L loads piece L (timing only: wrong CRCs)
 constexpr int kRowsAblNoStore = 16;     // results never stored (timing / codegen only)
+constexpr int kRowsAblNoTranspose = 32; // skip the permlane transposes (timing only)
+constexpr int kRowsAblLdsSeed = 64;     // QB = 1 seeds from LDS TQ16 (+ ZI) instead of scalar loads (exact)
+constexpr int kRowsAblNoFastLoad = 128; // always the per-lane address path (exact)
 
 namespace rows {
 
@@ -214,21 +262,36 @@ __device__ __forceinline__ uint32_t xor_fold(const u32x4 (&p)[4]) {
   return r;
 }
 
-// Per-row merge (see header): ST1 per lane, reduce over lo (lane bits 0-3),
-// then for QB = 1 ST2 per 16-lane row and reduce over hi (lane bits 4-5).
-template <int QB>
-__device__ __forceinline__ uint32_t merge(const uint8_t *lds, uint32_t s, uint32_t st1_base, uint32_t st2_base) {
-  s = nib_map<2048u, 7u>(lds, s, st1_base); // A_{64*(15-lo)}
+// Merge step 1 (see header): ST1 per lane, then XOR over lo (lane bits 0-3).
+// Every lane of 16-lane row hi then holds v_hi = crc0 of quarter hi.
+__device__ __forceinline__ uint32_t merge_lo(const uint8_t *lds, uint32_t s, uint32_t lsel1) {
+  s = st1_map(lds, s, lsel1); // A_{64*(15-lo)}
   s ^= dpp_xor1(s);
   s ^= dpp_xor2(s);
   s ^= dpp_ror4(s);
-  s ^= dpp_ror8(s);
-  if constexpr (QB == 1) {
-    s = nib_map<256u, 4u>(lds, s, st2_base); // A_{1024*(3-hi)}
-    s = xor_lanebit4(s);
-    s = xor_lanebit5(s);
-  }
-  return s;
+  return s ^ dpp_ror8(s);
+}
+
+// Merge step 2 for QB = 1 fused with the Horner step of the previous rows:
+// one ds_read per lane serves both the per-quarter ST2 shift A_{1024*(3-hi)}
+// of v_hi (lanes lo < 8, nibble lo) and RW(u) = A_4096(u) of the wave-uniform
+// running CRC u (lanes 8..15 of row 0, nibble lo - 8); other lanes read zero.
+// After dist_reduce8 and the hi reduction, lane 4 holds crc0(row) and lane 12
+// holds A_4096(u).
+struct RowMerge {
+  uint32_t crc;  // crc0 of the 4 KiB row (uniform)
+  uint32_t rwu;  // A_4096(u) (uniform)
+};
+__device__ __forceinline__ RowMerge merge_row(const uint8_t *lds, uint32_t v, uint32_t u, const DistLane &d) {
+  const uint32_t src = d.own ? v : u;
+  const uint32_t nib = (src >> d.shift) & 15u;
+  uint32_t t = dist_reduce8(lds_ld(lds, d.row_base + nib * d.row_mul));
+  t = xor_lanebit4(t);
+  t = xor_lanebit5(t);
+  RowMerge m;
+  m.crc = (uint32_t)__builtin_amdgcn_readlane((int)t, 4);
+  m.rwu = (uint32_t)__builtin_amdgcn_readlane((int)t, 12);
+  return m;
 }
 
 struct QuarterInfo {
@@ -273,12 +336,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t lane4 = (lane & 31u) * 4u;
-  const uint32_t lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);
+  const uint32_t lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);  // MAIN tables
+  const uint32_t lsel1 = lane4 | ((lane4 + 128u) << 8) | (2u << 16); // ST1
   const uint32_t hi = lane >> 4;                   // 16-lane row = quarter after the transpose
   // byte offset of this lane's piece in a quarter
   const uint32_t pofs = 16u * (((ABL & kRowsAblNaturalOrder) != 0) ? lane : piece_of_lane(lane));
-  const uint32_t st1_base = kLdsST1 + lane4;
-  const uint32_t st2_base = kLdsST2 + hi * 4u;
+  const DistLane dl = dist_lane(lane);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * 16u;
   // Tasks (QB = 1: items, QB = 4: groups of 4 items) are dealt round-robin:
@@ -304,18 +367,23 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       buf[b] = u32x4{v, v ^ 0x5bd1e995u, v + 0x68e31da4u, ~v};
     }
   };
-  auto row_crc = [&](u32x4 (&buf)[4]) -> uint32_t {
-    transpose(buf);
+  // Transpose + chain + merge step 1: every lane of 16-lane row hi returns
+  // crc0 of quarter hi of the row.
+  auto quarter_crcs = [&](u32x4 (&buf)[4]) -> uint32_t {
+    if constexpr ((ABL & kRowsAblNoTranspose) == 0) transpose(buf);
     uint32_t s;
     if constexpr ((ABL & kRowsAblNoCompute) != 0) s = xor_fold(buf);
     else s = seg_crc(lds, buf, lsel);
-    if constexpr ((ABL & kRowsAblNoMerge) == 0) s = merge<QB>(lds, s, st1_base, st2_base);
+    if constexpr ((ABL & kRowsAblNoMerge) == 0) s = merge_lo(lds, s, lsel1);
     return s;
   };
 
   if constexpr (QB == 1) {
     // Item metadata (wave-uniform).  item must be < n.
-    auto meta = [&](uint64_t item, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &nr) {
+    // The zlib seed A_first(0xFFFFFFFF) of the item's first row is a scalar
+    // load from the global Tq table, issued here -- a task ahead of its use.
+    auto meta = [&](uint64_t item, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &nr,
+                    uint32_t &seed) {
       const uint64_t off = a.offsets ? ld_const(a.offsets, item) : item * a.stride;
       len = a.lengths ? ld_const(a.lengths, item) : a.len;
       p0 = (uint64_t)(uintptr_t)a.base + off;
@@ -323,21 +391,33 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       lp = (uint64_t)len + z;
       const uint64_t rows_ = (lp + kRow - 1) / kRow;
       nr = rows_ ? (uint32_t)rows_ : 1u; // zero-length items: one fully masked row
+      if constexpr ((ABL & kRowsAblLdsSeed) != 0)
+        seed = (uint32_t)(lp - (uint64_t)(nr - 1) * kRow); // resolved in compute
+      else
+        seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, (uint32_t)(lp - (uint64_t)(nr - 1) * kRow));
     };
     auto issue = [&](uint64_t p0, uint64_t lp, uint32_t nr, uint32_t r, bool ok, uint64_t safe, u32x4 (&buf)[4]) {
       if constexpr ((ABL & kRowsAblNoLoad) != 0) {
         synth(p0 + r, buf);
       } else {
         const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
+        if (ok && rs >= 0 && (ABL & kRowsAblNoFastLoad) == 0) {
+          // Whole row inside the item: scalar row base + the lane's constant
+          // piece offset + immediate quarter offsets (no per-lane address math).
+          const uint8_t *row = reinterpret_cast<const uint8_t *>(p0 + (uint64_t)rs);
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int64_t v = rs + b * kQuarter + (int64_t)pofs;
-          const uint64_t src = (ok && v + 16 > 0) ? p0 + (uint64_t)v : safe;
-          buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
+          for (int b = 0; b < 4; ++b) buf[b] = ld16<NT>(row + pofs + b * kQuarter);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int64_t v = rs + b * kQuarter + (int64_t)pofs;
+            const uint64_t src = (ok && v + 16 > 0) ? p0 + (uint64_t)v : safe;
+            buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
+          }
         }
       }
     };
-    uint32_t W = 0;
+    uint32_t W = 0; // running crc0 (Horner over rows) of the current item, wave-uniform
     // Finished CRCs are parked in one VGPR (lane k = this wave's k-th pending
     // item, item = gw + (j0 + k) * nwaves) and stored 64 at a time: a per-row
     // store would make the compiler drain vmcnt (store-data WAR) every row.
@@ -357,7 +437,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       outv = (lane == ocount) ? res : outv;
       if (++ocount == 64u) flush();
     };
-    auto compute = [&](bool valid, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r,
+    auto compute = [&](bool valid, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
                        u32x4 (&buf)[4]) {
       const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
       const bool last = r + 1 == nr;
@@ -365,17 +445,27 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) buf[b] = mask_piece(buf[b], rs + b * kQuarter + (int64_t)pofs, len);
       }
-      const uint32_t s = row_crc(buf);
-      if (r == 0) {
-        const uint32_t first = (uint32_t)(lp - (uint64_t)(nr - 1) * kRow);
-        W = (mode == kModeRaw) ? 0u : seed_for(lds, first);
+      const uint32_t v = quarter_crcs(buf);
+      RowMerge m;
+      if constexpr ((ABL & kRowsAblNoMerge) == 0) {
+        m = merge_row(lds, v, W, dl);
       } else {
-        W = nib_map<64u, 2u>(lds, W, kLdsRW2);
+        m.crc = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        m.rwu = W;
       }
-      W ^= s;
+      // Horner over rows: A_4096(W), or the zlib seed on the item's first row.
+      if constexpr ((ABL & kRowsAblLdsSeed) != 0) {
+        if (r == 0) {
+          const uint32_t first = seed, up = (first + 15u) & ~15u;
+          uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
+          if (up != first) w = dist_uniform(lds, w, kLdsZI2 + (up - first - 1u) * 512u, dl);
+          seed = (mode == kModeRaw) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
+        }
+      }
+      W = ((r == 0) ? seed : m.rwu) ^ m.crc;
       if (last) {
         uint32_t res = W;
-        if (z != 0) res = nib_map<64u, 2u>(lds, res, kLdsZI2 + (z - 1u) * 512u);
+        if (z != 0) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
         if (mode == kModeFinal) res = ~res;
         if (valid) park(res);
       }
@@ -383,18 +473,19 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 
     uint64_t c_item = gw;
     uint64_t c_p0, c_lp;
-    uint32_t c_len, c_z, c_nr, c_r = 0;
-    meta(c_item, c_p0, c_lp, c_len, c_z, c_nr);
+    uint32_t c_len, c_z, c_nr, c_seed, c_r = 0;
+    meta(c_item, c_p0, c_lp, c_len, c_z, c_nr, c_seed);
     const uint64_t safe = c_p0 & ~(uint64_t)15; // 16-B block holding this wave's first byte
     // Successor of task (item, r) with metadata nr: same item next row, or the
     // wave's next item.  Invalid successors carry the wave's first item's
     // (in-range) metadata and load from `safe`; their results are dropped.
     auto succ = [&](bool ok, uint64_t item, uint32_t r, uint32_t nr, uint64_t &s_item, uint32_t &s_r,
-                    bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr) {
+                    bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr,
+                    uint32_t &seed) {
       const bool adv = r + 1 < nr;
       s_item = adv ? item : item + nwaves;
       s_ok = ok && s_item < n;
-      meta(s_ok ? s_item : gw, p0, lp, len, z, snr);
+      meta(s_ok ? s_item : gw, p0, lp, len, z, snr, seed);
       s_r = adv ? r + 1 : 0u;
     };
     // The unrolled loops have ONE exit, at the bottom: a mid-body break edge
@@ -409,12 +500,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
         uint64_t m_item, m_p0, m_lp;
-        uint32_t m_r, m_len, m_z, m_nr;
+        uint32_t m_r, m_len, m_z, m_nr, m_seed;
         bool m_ok;
-        succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr);
+        succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, cb);
         c_ok = m_ok;
+        c_seed = m_seed;
         c_item = m_item;
         c_r = m_r;
         c_p0 = m_p0;
@@ -431,19 +523,21 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       // DEPTH = 2: the next two rows' loads are in flight while one computes.
       u32x4 bufA[4], bufB[4], bufC[4];
       uint64_t n_item, n_p0, n_lp;
-      uint32_t n_r, n_len, n_z, n_nr;
+      uint32_t n_r, n_len, n_z, n_nr, n_seed;
       bool n_ok;
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      succ(true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_p0, n_lp, n_len, n_z, n_nr);
+      succ(true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_p0, n_lp, n_len, n_z, n_nr, n_seed);
       issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) {
         uint64_t m_item, m_p0, m_lp;
-        uint32_t m_r, m_len, m_z, m_nr;
+        uint32_t m_r, m_len, m_z, m_nr, m_seed;
         bool m_ok;
-        succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr);
+        succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, cb);
         c_ok = n_ok;
+        c_seed = n_seed;
+        n_seed = m_seed;
         c_item = n_item;
         c_r = n_r;
         c_lp = n_lp;
@@ -484,18 +578,37 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       r.vstart = (int64_t)r.len + r.z - (int64_t)kQuarter;
       return r;
     };
-    auto issue = [&](uint64_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) {
+    // issue() also returns this row's zlib seeds A_{len_b+z_b}(0xFFFFFFFF),
+    // lane-selected by quarter: scalar loads from the global Tq table issued a
+    // row ahead of their use.
+    auto issue = [&](uint64_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) -> uint32_t {
+      QuarterInfo qi[4];
+      bool full = ok;
+      uint32_t sl = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        qi[b] = quarter(g, b);
+        full = full && qi[b].vstart == 0 && qi[b].len != 0;
+        const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, qi[b].len + qi[b].z);
+        sl = (hi == (uint32_t)b) ? seed : sl;
+      }
       if constexpr ((ABL & kRowsAblNoLoad) != 0) {
         synth(g, buf);
       } else {
+        if (full) { // four whole 1 KiB items: scalar bases, constant lane offset
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const QuarterInfo qi = quarter(g, b);
-          const int64_t v = qi.vstart + (int64_t)pofs;
-          const uint64_t src = (ok && qi.len != 0 && v + 16 > 0) ? (uint64_t)(uintptr_t)qi.p0 + (uint64_t)v : safe;
-          buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
+          for (int b = 0; b < 4; ++b) buf[b] = ld16<NT>(qi[b].p0 + pofs);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int64_t v = qi[b].vstart + (int64_t)pofs;
+            const uint64_t src =
+                (ok && qi[b].len != 0 && v + 16 > 0) ? (uint64_t)(uintptr_t)qi[b].p0 + (uint64_t)v : safe;
+            buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
+          }
         }
       }
+      return sl;
     };
     // Parked results: lane k = item 4 * (gw + (j0 + k / 4) * nwaves) + k % 4 (see QB = 1).
     uint32_t outv = 0, ocount = 0;
@@ -506,27 +619,31 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       j0 += ocount / 4u;
       ocount = 0;
     };
-    auto compute = [&](uint64_t g, u32x4 (&buf)[4]) {
-      uint32_t z = 0, len = 0;
+    auto compute = [&](uint64_t g, uint32_t sl, u32x4 (&buf)[4]) {
+      uint32_t zq[4], lq[4], zl = 0, zany = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const QuarterInfo qi = quarter(g, b);
         if (qi.vstart < 0 || qi.z != 0 || qi.len == 0)
           buf[b] = mask_piece(buf[b], qi.vstart + (int64_t)pofs, qi.len);
-        if (hi == (uint32_t)b) {
-          z = qi.z;
-          len = qi.len;
-        }
+        zq[b] = qi.z;
+        lq[b] = qi.len;
+        zany |= qi.z;
+        zl = (hi == (uint32_t)b) ? qi.z : zl;
       }
-      const uint32_t s = row_crc(buf); // lanes of 16-lane row b hold crc0 of item 4g+b
-      uint32_t res = (mode == kModeRaw) ? 0u : seed_for(lds, len + z);
-      res ^= s;
-      if (z != 0) res = nib_map<64u, 2u>(lds, res, kLdsZI2 + (z - 1u) * 512u);
+      uint32_t res = quarter_crcs(buf) ^ sl; // 16-lane row b: item 4g+b
+      if (zany != 0) {
+        // Undo the z_b pad bytes of each row's item: distributed nibble step
+        // within each row (rows with z_b = 0 keep res; their lookup hits RW2).
+        const uint32_t nib = (res >> dl.shift) & 15u;
+        const uint32_t t = dist_reduce8(lds_ld(lds, kLdsZI2 + (zl - 1u) * 512u + dl.n64 + nib * 4u));
+        res = (zl != 0u) ? t : res; // valid in lanes 4..7 of each row
+      }
       if (mode == kModeFinal) res = ~res;
-      if (len == 0) res = 0u;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const uint32_t v = __builtin_amdgcn_readlane(res, 16 * b);
+        uint32_t v = __builtin_amdgcn_readlane(res, 16 * b + 4);
+        if (lq[b] == 0) v = 0u;
         outv = (lane == ocount + (uint32_t)b) ? v : outv;
       }
       ocount += 4;
@@ -536,12 +653,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
-      issue(g, true, safe, bufA);
+      uint32_t c_sl = issue(g, true, safe, bufA);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
         const uint64_t ng = g + nwaves;
         const bool ok = ng < ngroups;
-        issue(ok ? ng : g, ok, safe, nb);
-        compute(g, cb);
+        const uint32_t n_sl = issue(ok ? ng : g, ok, safe, nb);
+        compute(g, c_sl, cb);
+        c_sl = n_sl;
         g = ng;
         return ok;
       };
@@ -551,16 +669,18 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
-      issue(g, true, safe, bufA);
+      uint32_t c_sl = issue(g, true, safe, bufA), n_sl;
       {
         const uint64_t g1 = g + nwaves;
-        issue(g1 < ngroups ? g1 : g, g1 < ngroups, safe, bufB);
+        n_sl = issue(g1 < ngroups ? g1 : g, g1 < ngroups, safe, bufB);
       }
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
         const uint64_t g2 = g + 2 * nwaves;
         const bool ok2 = g2 < ngroups;
-        issue(ok2 ? g2 : g, ok2, safe, fb);
-        compute(g, cb);
+        const uint32_t m_sl = issue(ok2 ? g2 : g, ok2, safe, fb);
+        compute(g, c_sl, cb);
+        c_sl = n_sl;
+        n_sl = m_sl;
         g += nwaves;
         return g < ngroups;
       };

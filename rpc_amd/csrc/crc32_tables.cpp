@@ -86,7 +86,8 @@ void build_lds_image_v2(uint32_t *img) {
   for (uint32_t c = 0; c < 32; ++c) { // lo = c & 15
     nibble_table(64u * (15u - (c & 15u)), nt);
     for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsST1 + n * 2048 + nib * 128 + c * 4, nt[n][nib]);
+      for (uint32_t nib = 0; nib < 16; ++nib)
+        put(kLdsST1 + (n >> 1) * 4096 + nib * 256 + (n & 1) * 128 + c * 4, nt[n][nib]);
   }
   for (uint32_t hi = 0; hi < 4; ++hi) {
     nibble_table(1024u * (3u - hi), nt);

@@ -1,8 +1,10 @@
 // tests/cpu_emu/rows_emu.cpp -- CPU emulation of crc32_rows_kernel lane by lane
 // (TEST CODE): permuted coalesced piece loads, the v_permlane16/32_swap
-// transpose, the slice-by-4 chain on the rows LDS image, ST1/ST2 nibble steps
-// with the exact DPP quad/row_ror and permlane-swap reductions, Horner, Tq, ZI.  Compared with the oracle by
-// tests/test_kernel_emu.py.  Not the product path.
+// transpose, the slice-by-4 chain on the rows LDS image, the perm-addressed
+// ST1 step with the exact DPP quad/row_ror reductions, the distributed
+// ST2 + Horner step (row_shr 4 with zero fill, permlane-swap reductions,
+// readlane 4 / 12), global Tq seeds and the distributed ZI steps.  Compared
+// with the oracle by tests/test_kernel_emu.py.  Not the product path.
 //
 // stdin:  QB misalign n  then n lengths; bodies are splitmix bytes (seed 7)
 //         back to back from byte `misalign` of a 16-aligned buffer.
@@ -37,11 +39,6 @@ static uint32_t slice4(uint32_t x, uint32_t lsel) {
   return ld(perm(x, lsel, 0x0C0C0400u)) ^ ld(perm(x, lsel, 0x0C0C0501u)) ^ ld(perm(x, lsel, 0x0C020600u)) ^
          ld(perm(x, lsel, 0x0C020701u));
 }
-static uint32_t nib_map(uint32_t s, uint32_t base, uint32_t stride, uint32_t shift) {
-  uint32_t r = 0;
-  for (uint32_t n = 0; n < 8; ++n) r ^= ld(base + n * stride + (((s >> (4 * n)) & 15u) << shift));
-  return r;
-}
 typedef uint32_t Wave[64];
 static void quad_perm(const Wave in, Wave out, const int p[4]) {
   for (int l = 0; l < 64; ++l) out[l] = in[(l & ~3) | p[l & 3]];
@@ -49,17 +46,27 @@ static void quad_perm(const Wave in, Wave out, const int p[4]) {
 static void row_ror(const Wave in, Wave out, int n) { // dst[i] = src[(i - n) mod 16] within each row
   for (int l = 0; l < 64; ++l) out[l] = in[(l & ~15) | (((l & 15) - n) & 15)];
 }
-static void lane_xor(const Wave in, Wave out, int m) {
-  for (int l = 0; l < 64; ++l) out[l] = in[l ^ m];
+static void row_shr_zero(const Wave in, Wave out, int n) { // dst[i] = src[i - n] within the row, else 0
+  for (int l = 0; l < 64; ++l) out[l] = ((l & 15) >= n) ? in[l - n] : 0u;
+}
+// dist_reduce8: quad xor1, quad xor2, row_shr 4 (zero fill), each XORed in.
+static void dist_reduce8(Wave t) {
+  static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
+  Wave u;
+  quad_perm(t, u, px1); for (int l = 0; l < 64; ++l) t[l] ^= u[l];
+  quad_perm(t, u, px2); for (int l = 0; l < 64; ++l) t[l] ^= u[l];
+  row_shr_zero(t, u, 4); for (int l = 0; l < 64; ++l) t[l] ^= u[l];
 }
 
 struct Piece { uint32_t d[4]; };
 
-static uint32_t seed_for(uint32_t first) {
-  uint32_t up = (first + 15u) & ~15u;
-  uint32_t w = ld(kLdsTQ16 + up / 4u);
-  if (up != first) w = nib_map(w, kLdsZI2 + (up - first - 1u) * 512u, 64, 2);
-  return w;
+// dist_uniform: lane n = lane & 7 looks up nibble n of the uniform u in a
+// [n][nib] table; the result is read from lane 4.
+static uint32_t dist_uniform(uint32_t u, uint32_t table) {
+  Wave t;
+  for (int l = 0; l < 64; ++l) t[l] = ld(table + (uint32_t)(l & 7) * 64u + ((u >> (4 * (l & 7))) & 15u) * 4u);
+  dist_reduce8(t);
+  return t[4];
 }
 
 static uint32_t piece_of_lane(uint32_t L) { return ((L & 15u) << 2) | (L >> 4); }
@@ -113,11 +120,21 @@ static void xor_lanebit(Wave s, int bit) {
   for (int l = 0; l < 64; ++l) s[l] = a[l] ^ b[l];
 }
 
-// ST1 step + reduce over lane bits 0-3 (quad_perm xor1, xor2, row_ror 4, 8).
+// ST1 (perm-addressed) + reduce over lane bits 0-3 (quad_perm xor1, xor2, row_ror 4, 8).
+static uint32_t st1_map(uint32_t s, uint32_t lane) {
+  const uint32_t lane4 = (lane & 31u) * 4u, lsel1 = lane4 | ((lane4 + 128u) << 8) | (2u << 16);
+  const uint32_t xl = s & 0x0F0F0F0Fu, xh = (s >> 4) & 0x0F0F0F0Fu;
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    r ^= ld(perm(xl, lsel1, 0x0C020400u + (k << 8)) + k * 4096u);
+    r ^= ld(perm(xh, lsel1, 0x0C020401u + (k << 8)) + k * 4096u);
+  }
+  return r;
+}
 static void merge_lo(Wave s) {
   static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
   Wave t;
-  for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsST1 + (uint32_t)(l & 31) * 4u, 2048, 7);
+  for (int l = 0; l < 64; ++l) s[l] = st1_map(s[l], (uint32_t)l);
   quad_perm(s, t, px1); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
   quad_perm(s, t, px2); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
   row_ror(s, t, 4); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
@@ -161,15 +178,26 @@ static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
     Wave s;
     row_chain(P, s);
     merge_lo(s);
-    for (int l = 0; l < 64; ++l) s[l] = nib_map(s[l], kLdsST2 + (uint32_t)(l >> 4) * 4u, 256, 4);
-    xor_lanebit(s, 4);
-    xor_lanebit(s, 5);
-    uint32_t rowcrc = s[0];
-    for (int l = 1; l < 64; ++l) if (s[l] != rowcrc) { fprintf(stderr, "reduction not uniform\n"); exit(4); }
-    W = (r == 0) ? seed_for(first) : nib_map(W, kLdsRW2, 64, 2);
-    W ^= rowcrc;
+    for (int h = 0; h < 4; ++h)
+      for (int l = 16 * h; l < 16 * h + 16; ++l)
+        if (s[l] != s[16 * h]) { fprintf(stderr, "row not uniform\n"); exit(4); }
+    // distributed ST2 (lanes lo < 8, own row value) + RW of W (row 0, lanes 8..15)
+    Wave t;
+    for (int l = 0; l < 64; ++l) {
+      const uint32_t lo = l & 15, hi = l >> 4;
+      const bool own = lo < 8;
+      const uint32_t base = own ? kLdsST2 + lo * 256u + hi * 4u : (hi == 0 ? kLdsRW2 + (lo - 8u) * 64u : kLdsZero);
+      const uint32_t mul = own ? 16u : (hi == 0 ? 4u : 0u);
+      const uint32_t src = own ? s[l] : W;
+      t[l] = ld(base + ((src >> (4 * (l & 7))) & 15u) * mul);
+    }
+    dist_reduce8(t);
+    xor_lanebit(t, 4);
+    xor_lanebit(t, 5);
+    const uint32_t rowcrc = t[4], rwu = t[12];
+    W = ((r == 0) ? g_tq[first] : rwu) ^ rowcrc;
   }
-  if (z) W = nib_map(W, kLdsZI2 + (z - 1) * 512, 64, 2);
+  if (z) W = dist_uniform(W, kLdsZI2 + (z - 1) * 512);
   return ~W;
 }
 
@@ -182,7 +210,7 @@ static void emu_qb4(const uint8_t *const p0[4], const uint32_t len[4], int nvali
     const uint8_t *q = b < nvalid ? p0[b] : p0[0];
     z[b] = (uint32_t)(0u - (uint32_t)(uintptr_t)(q + L)) & 15u;
     int64_t vstart = (int64_t)L + z[b] - 1024;
-    w0[b] = L == 0 ? 0u : seed_for(L + z[b]);
+    w0[b] = g_tq[L + z[b]];
     for (int Ln = 0; Ln < 64; ++Ln) {
       int64_t v = vstart + 16 * (int64_t)piece_of_lane((uint32_t)Ln);
       P[b][Ln] = (b < nvalid && L != 0 && v + 16 > 0) ? load_piece(q + v) : Piece{{0, 0, 0, 0}};
@@ -192,14 +220,25 @@ static void emu_qb4(const uint8_t *const p0[4], const uint32_t len[4], int nvali
   Wave s;
   row_chain(P, s);
   merge_lo(s);
-  for (int h = 0; h < 4; ++h) {
+  for (int h = 0; h < 4; ++h)
     for (int l = 16 * h; l < 16 * h + 16; ++l)
       if (s[l] != s[16 * h]) { fprintf(stderr, "row not uniform\n"); exit(4); }
-    uint32_t res = w0[h] ^ s[16 * h];
-    if (z[h]) res = nib_map(res, kLdsZI2 + (z[h] - 1) * 512, 64, 2);
-    res = ~res;
-    if (h >= nvalid || len[h] == 0) res = 0;
-    out[h] = res;
+  Wave res;
+  for (int l = 0; l < 64; ++l) res[l] = w0[l >> 4] ^ s[l];
+  if (z[0] | z[1] | z[2] | z[3]) {
+    Wave t;
+    for (int l = 0; l < 64; ++l) {
+      const uint32_t zl = z[l >> 4];
+      const uint32_t table = kLdsZI2 + (zl - 1u) * 512u; // zl = 0: lands in RW2, discarded
+      t[l] = ld(table + (uint32_t)(l & 7) * 64u + ((res[l] >> (4 * (l & 7))) & 15u) * 4u);
+    }
+    dist_reduce8(t);
+    for (int l = 0; l < 64; ++l) if (z[l >> 4]) res[l] = t[l];
+  }
+  for (int h = 0; h < 4; ++h) {
+    uint32_t r = ~res[16 * h + 4];
+    if (h >= nvalid || len[h] == 0) r = 0;
+    out[h] = r;
   }
 }
 

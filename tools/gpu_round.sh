@@ -8,6 +8,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift || true
 STEPS=${*:-"smoke tests bench probe prof"}
+SUSTAIN=${SUSTAIN:-product,stream_nt1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl4_d1}
+ABLATE=${ABLATE:-qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl4_d1}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 run() { # name timeout cmd...
@@ -27,9 +29,9 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py ;;
     probe) run probe 600 python tools/probe.py ;;
     ablate) run ablate 600 python tools/probe.py --mode ablate --rounds 3 ;;
-    ablate_nat) run ablate_nat 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2,qb1_pair1_nt1_abl3_d2,qb1_pair1_nt1_abl16_d1 ;;
-    sustain) run sustain 600 python tools/probe.py --mode sustain --launches 60 --only product,stream_nt1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2 ;;
-    ablate_c1) run ablate_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 ;;
+    ablate_nat) run ablate_nat 600 python tools/probe.py --mode ablate --rounds 3 --only $ABLATE ;;
+    sustain) run sustain 600 python tools/probe.py --mode sustain --launches 1500 --smi-out $OUT/smi.jsonl --only $SUSTAIN ;;
+    ablate_c1) run ablate_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 --only qb4_pair1_nt1_abl0_d1,qb4_pair1_nt1_abl3_d1,qb4_pair1_nt1_abl4_d1,qb4_pair1_nt1_abl0_d2 ;;
     bench_c1) run bench_c1 600 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive ;;
     bench_c2) run bench_c2 600 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;

@@ -76,7 +76,8 @@ def ablate_variants(w, a):
     combos = [(1, 1, 1, 0, 1), (1, 1, 0, 0, 1), (1, 1, 1, 1, 1), (1, 1, 1, 2, 1), (1, 1, 1, 3, 1), (1, 1, 1, 4, 1),
               (1, 1, 1, 6, 1), (1, 1, 1, 0, 2), (1, 1, 0, 0, 2), (1, 1, 1, 3, 2),
               (1, 1, 1, 8, 1), (1, 1, 1, 11, 1), (1, 1, 1, 9, 1), (1, 1, 0, 11, 1), (1, 1, 0, 3, 1),
-              (1, 1, 1, 16, 1), (1, 1, 1, 19, 1)]
+              (1, 1, 1, 16, 1), (1, 1, 1, 19, 1), (1, 1, 1, 32, 1), (1, 1, 1, 35, 1), (1, 1, 1, 51, 1),
+              (1, 1, 1, 64, 1), (1, 1, 1, 128, 1), (1, 1, 1, 192, 1), (1, 1, 1, 67, 1), (1, 1, 1, 131, 1), (1, 1, 1, 195, 1)]
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
                    (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)]
@@ -89,7 +90,7 @@ def ablate_variants(w, a):
     torch.cuda.synchronize()
     ref = w.out.clone()
     for c in combos:
-        if c[3] == 0:
+        if c[3] & ~192 == 0:  # exact variants (seed source / load path only)
             mk(*c)()
             torch.cuda.synchronize()
             assert torch.equal(out, ref), c
@@ -158,11 +159,19 @@ def sustain(w, a):
                           "last_quarter_us": round(statistics.mean(d[-q:]), 1),
                           "min_us": round(min(d), 1), "max_us": round(max(d), 1),
                           "mean_GBps": round(nb / (statistics.mean(d) / 1e6) / 1e9, 1),
-                          "per_launch_us": [round(x, 1) for x in d]}), flush=True)
+                          "per_launch_us": [round(x, 1) for x in d[::max(1, len(d) // 40)]]}), flush=True)
     stop.set()
     th.join(timeout=15)
+    import re
     for t, out in smi_log:
-        print(json.dumps({"smi_t_s": t, "out": out.strip()[-600:]}))
+        # GFX clocks (per XCD) and socket power, whatever the tool's layout
+        gfx = [int(m) for m in re.findall(r"GFX_\d+:\s*\n\s*CLK:\s*(\d+)", out)]
+        pw = re.findall(r"(?:SOCKET_POWER|POWER_USAGE|Current Socket Graphics Package Power \(W\)):?\s*([\d.]+)", out)
+        print(json.dumps({"smi_t_s": t, "gfx_mhz": gfx, "power_w": pw[:2]}))
+    if a.smi_out and smi_log:
+        with open(a.smi_out, "w") as f:
+            for t, out in smi_log:
+                f.write(json.dumps({"t": t, "out": out}) + "\n")
 
 
 def main():
@@ -173,6 +182,7 @@ def main():
     ap.add_argument("--grids", default="0,512,1024")
     ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain"])
     ap.add_argument("--launches", type=int, default=60)
+    ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
     a = ap.parse_args()
     torch.cuda.set_device(0)

@@ -56,7 +56,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows(const uint8_t *
   a.out = d_out;
   hipStream_t s = static_cast<hipStream_t>(stream);
   V(1, 1, 0, 1) V(1, 0, 0, 1) V(1, 1, 1, 1) V(1, 1, 2, 1) V(1, 1, 3, 1) V(1, 1, 4, 1) V(1, 1, 6, 1)
-  V(1, 1, 0, 2) V(1, 0, 0, 2) V(1, 1, 3, 2) V(1, 1, 8, 1) V(1, 1, 11, 1) V(1, 1, 9, 1) V(1, 0, 11, 1) V(1, 0, 3, 1) V(1, 1, 16, 1) V(1, 1, 19, 1)
+  V(1, 1, 0, 2) V(1, 0, 0, 2) V(1, 1, 3, 2) V(1, 1, 8, 1) V(1, 1, 11, 1) V(1, 1, 9, 1) V(1, 0, 11, 1) V(1, 0, 3, 1) V(1, 1, 16, 1) V(1, 1, 19, 1) V(1, 1, 32, 1) V(1, 1, 35, 1) V(1, 1, 51, 1) V(1, 1, 64, 1) V(1, 1, 128, 1) V(1, 1, 192, 1) V(1, 1, 67, 1) V(1, 1, 131, 1) V(1, 1, 195, 1)
   V(4, 1, 0, 1) V(4, 0, 0, 1) V(4, 1, 3, 1) V(4, 1, 4, 1) V(4, 1, 6, 1) V(4, 1, 0, 2) V(4, 1, 3, 2)
   return -22;
 }
