@@ -123,17 +123,23 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   uint64_t blocks = (waves + kWaves - 1) / kWaves;
   if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
   const dim3 grid((unsigned)blocks), block(kWaves * 64);
+  const bool ragged = a.offsets != nullptr;
+  if (ragged != (a.lengths != nullptr)) return hipErrorInvalidValue;
+#define RPCCRC_ROWS(Q, N, R) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R>), grid, block, 0, stream, a)
   if (QB == 4) {
-    if (nt)
-      hipLaunchKernelGGL((crc32_rows_kernel<4, true>), grid, block, 0, stream, a);
-    else
-      hipLaunchKernelGGL((crc32_rows_kernel<4, false>), grid, block, 0, stream, a);
+    if (ragged) {
+      if (nt) RPCCRC_ROWS(4, true, true); else RPCCRC_ROWS(4, false, true);
+    } else {
+      if (nt) RPCCRC_ROWS(4, true, false); else RPCCRC_ROWS(4, false, false);
+    }
   } else {
-    if (nt)
-      hipLaunchKernelGGL((crc32_rows_kernel<1, true>), grid, block, 0, stream, a);
-    else
-      hipLaunchKernelGGL((crc32_rows_kernel<1, false>), grid, block, 0, stream, a);
+    if (ragged) {
+      if (nt) RPCCRC_ROWS(1, true, true); else RPCCRC_ROWS(1, false, true);
+    } else {
+      if (nt) RPCCRC_ROWS(1, true, false); else RPCCRC_ROWS(1, false, false);
+    }
   }
+#undef RPCCRC_ROWS
   return hipGetLastError();
 }
 

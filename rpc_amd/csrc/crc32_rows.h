@@ -309,7 +309,9 @@ struct QuarterInfo {
 // exactly 4 loads and 1 store so the compiler can count vmcnt exactly (the
 // prefetch is never drained early).  Per-task state is plain wave-uniform
 // scalars (SGPRs); item metadata comes from scalar loads.
-template <int QB, bool NT, int ABL = 0, int DEPTH = 1>
+// RAGGED: items come from the offsets / lengths arrays (both non-null);
+// otherwise item i is [base + i * stride, + len).
+template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1>
 __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
@@ -384,8 +386,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // load from the global Tq table, issued here -- a task ahead of its use.
     auto meta = [&](uint64_t item, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &nr,
                     uint32_t &seed) {
-      const uint64_t off = a.offsets ? ld_const(a.offsets, item) : item * a.stride;
-      len = a.lengths ? ld_const(a.lengths, item) : a.len;
+      const uint64_t off = RAGGED ? ld_const(a.offsets, item) : item * a.stride;
+      len = RAGGED ? ld_const(a.lengths, item) : a.len;
       p0 = (uint64_t)(uintptr_t)a.base + off;
       z = (uint32_t)(0u - (uint32_t)(p0 + len)) & 15u;
       lp = (uint64_t)len + z;
@@ -570,27 +572,34 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       const uint64_t item = 4 * g + b;
       const bool ok = item < n;
       const uint64_t it = ok ? item : 0;
-      const uint64_t off = a.offsets ? ld_const(a.offsets, it) : it * a.stride;
-      const uint32_t len = a.lengths ? ld_const(a.lengths, it) : a.len;
+      const uint64_t off = RAGGED ? ld_const(a.offsets, it) : it * a.stride;
+      const uint32_t len = RAGGED ? ld_const(a.lengths, it) : a.len;
       r.len = ok ? len : 0u;
       r.p0 = a.base + off;
       r.z = (uint32_t)(0u - (uint32_t)(uintptr_t)(r.p0 + r.len)) & 15u;
       r.vstart = (int64_t)r.len + r.z - (int64_t)kQuarter;
       return r;
     };
-    // issue() also returns this row's zlib seeds A_{len_b+z_b}(0xFFFFFFFF),
-    // lane-selected by quarter: scalar loads from the global Tq table issued a
-    // row ahead of their use.
-    auto issue = [&](uint64_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) -> uint32_t {
+    // issue() loads group g's row and returns what compute() needs, so item
+    // metadata is read once per group, a row ahead of its use: per quarter
+    // lz[b] = (len << 4) | z (len 0 = no item), and the lane-selected zlib
+    // seeds A_{len_b+z_b}(0xFFFFFFFF) (scalar loads from the global Tq table).
+    struct QuadMeta {
+      uint32_t lz[4];
+      uint32_t sl;
+    };
+    auto issue = [&](uint64_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) -> QuadMeta {
       QuarterInfo qi[4];
+      QuadMeta qm;
       bool full = ok;
-      uint32_t sl = 0;
+      qm.sl = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         qi[b] = quarter(g, b);
         full = full && qi[b].vstart == 0 && qi[b].len != 0;
+        qm.lz[b] = (qi[b].len << 4) | qi[b].z;
         const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, qi[b].len + qi[b].z);
-        sl = (hi == (uint32_t)b) ? seed : sl;
+        qm.sl = (hi == (uint32_t)b) ? seed : qm.sl;
       }
       if constexpr ((ABL & kRowsAblNoLoad) != 0) {
         synth(g, buf);
@@ -608,7 +617,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           }
         }
       }
-      return sl;
+      return qm;
     };
     // Parked results: lane k = item 4 * (gw + (j0 + k / 4) * nwaves) + k % 4 (see QB = 1).
     uint32_t outv = 0, ocount = 0;
@@ -619,19 +628,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       j0 += ocount / 4u;
       ocount = 0;
     };
-    auto compute = [&](uint64_t g, uint32_t sl, u32x4 (&buf)[4]) {
-      uint32_t zq[4], lq[4], zl = 0, zany = 0;
+    auto compute = [&](const QuadMeta &qm, u32x4 (&buf)[4]) {
+      uint32_t zl = 0, zany = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const QuarterInfo qi = quarter(g, b);
-        if (qi.vstart < 0 || qi.z != 0 || qi.len == 0)
-          buf[b] = mask_piece(buf[b], qi.vstart + (int64_t)pofs, qi.len);
-        zq[b] = qi.z;
-        lq[b] = qi.len;
-        zany |= qi.z;
-        zl = (hi == (uint32_t)b) ? qi.z : zl;
+        const uint32_t len = qm.lz[b] >> 4, z = qm.lz[b] & 15u;
+        const int64_t vstart = (int64_t)len + z - (int64_t)kQuarter;
+        if (vstart < 0 || z != 0 || len == 0) buf[b] = mask_piece(buf[b], vstart + (int64_t)pofs, len);
+        zany |= z;
+        zl = (hi == (uint32_t)b) ? z : zl;
       }
-      uint32_t res = quarter_crcs(buf) ^ sl; // 16-lane row b: item 4g+b
+      uint32_t res = quarter_crcs(buf) ^ qm.sl; // 16-lane row b: item 4g+b
       if (zany != 0) {
         // Undo the z_b pad bytes of each row's item: distributed nibble step
         // within each row (rows with z_b = 0 keep res; their lookup hits RW2).
@@ -643,7 +650,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         uint32_t v = __builtin_amdgcn_readlane(res, 16 * b + 4);
-        if (lq[b] == 0) v = 0u;
+        if ((qm.lz[b] >> 4) == 0) v = 0u;
         outv = (lane == ocount + (uint32_t)b) ? v : outv;
       }
       ocount += 4;
@@ -653,13 +660,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
-      uint32_t c_sl = issue(g, true, safe, bufA);
+      QuadMeta c_qm = issue(g, true, safe, bufA);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
         const uint64_t ng = g + nwaves;
         const bool ok = ng < ngroups;
-        const uint32_t n_sl = issue(ok ? ng : g, ok, safe, nb);
-        compute(g, c_sl, cb);
-        c_sl = n_sl;
+        const QuadMeta n_qm = issue(ok ? ng : g, ok, safe, nb);
+        compute(c_qm, cb);
+        c_qm = n_qm;
         g = ng;
         return ok;
       };
@@ -669,18 +676,18 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
-      uint32_t c_sl = issue(g, true, safe, bufA), n_sl;
+      QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
       {
         const uint64_t g1 = g + nwaves;
-        n_sl = issue(g1 < ngroups ? g1 : g, g1 < ngroups, safe, bufB);
+        n_qm = issue(g1 < ngroups ? g1 : g, g1 < ngroups, safe, bufB);
       }
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
         const uint64_t g2 = g + 2 * nwaves;
         const bool ok2 = g2 < ngroups;
-        const uint32_t m_sl = issue(ok2 ? g2 : g, ok2, safe, fb);
-        compute(g, c_sl, cb);
-        c_sl = n_sl;
-        n_sl = m_sl;
+        const QuadMeta m_qm = issue(ok2 ? g2 : g, ok2, safe, fb);
+        compute(c_qm, cb);
+        c_qm = n_qm;
+        n_qm = m_qm;
         g += nwaves;
         return g < ngroups;
       };

@@ -486,7 +486,7 @@ int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, con
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) return rc;
-  return items(*c, d_base, d_offsets, d_lengths, n, 0, 0, kModeFinal, d_out, 64,
+  return items(*c, d_base, d_offsets, d_lengths, n, 0, 0, kModeFinal, d_out, 1,
                static_cast<hipStream_t>(stream));
 }
 

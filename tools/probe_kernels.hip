@@ -28,7 +28,7 @@ int ensure_tables() {
 
 template <int QB, bool NT, int ABL, int DEPTH>
 void go(const ItemsArgs &a, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, ABL, DEPTH>), dim3(blocks), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, false, ABL, DEPTH>), dim3(blocks), dim3(1024), 0, s, a);
 }
 } // namespace
 
