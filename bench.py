@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     p.add_argument("--nontemporal", type=int, default=-1, help="-1 = library default")
+    p.add_argument("--ragged-path", default="auto", choices=["auto", "rows", "packed"],
+                   help="ragged-batch kernel (C2): packed = 1 KiB chunks four per row (default for n >= 64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
@@ -245,6 +247,7 @@ def main():
         dist.init_process_group("nccl", device_id=device)
     if args.nontemporal >= 0:
         rpc_amd.set_options(nontemporal=bool(args.nontemporal))
+    rpc_amd.set_ragged_path(args.ragged_path)
 
     w = Workload(args.config, rank, device)
     stream = torch.cuda.current_stream()
@@ -304,6 +307,7 @@ def main():
                 "workload": w.desc,
                 "bodies_per_gpu": w.n,
                 "body_len": w.L if w.kind != "ragged" else "log-uniform 64..65536",
+                "ragged_path": args.ragged_path if w.kind == "ragged" else None,
                 "bytes_per_gpu": w.total,
                 "parallelism": f"dp{world} (payload-index shards, RCCL barrier only)",
             },
@@ -314,7 +318,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / (HBM_PEAK_BPS / 1e9), 4),
                 "traffic": traffic,
-                "kernel": "crc32_rows_kernel" if w.kind != "large" else "crc32_rows_kernel (+chunk combine)",
+                "kernel": {"uniform": "crc32_rows_kernel",
+                           "ragged": "crc32_packed_kernel (+count/scan/plan)" if args.ragged_path != "rows"
+                           else "crc32_rows_kernel",
+                           "large": "crc32_rows_kernel (+chunk combine)"}[w.kind],
                 "avg_launch_us": round(kernel_s * 1e6, 2),
                 "algo_bytes_per_launch": w.algo_bytes,
             },

@@ -120,9 +120,21 @@ RPCCRC_API int rpc_crc32_fill_random_device(void *d_dst, uint64_t nbytes, uint64
  * lanes, 1 = the CRC kernel's 64-B-per-lane segments. */
 RPCCRC_API int rpc_crc32_stream_read_device(const void *d_src, uint64_t nbytes, int pattern, int nontemporal, void *stream);
 
-/* Tuning knobs (process-wide): nontemporal loads (0/1, default 0) and the
+/* Tuning knobs (process-wide): nontemporal loads (0/1, default 1) and the
  * persistent-grid size cap in workgroups (0 = one per CU). */
 RPCCRC_API int rpc_crc32_set_options(int nontemporal, int max_blocks);
+
+/* Kernel for ragged device batches (process-wide; used by rpc_crc32_device_batch,
+ * rpc_crc32_batch and the frames calls).  Results are identical either way.
+ *   RPCCRC_RAGGED_AUTO   packed for n >= 64 bodies, rows below (default)
+ *   RPCCRC_RAGGED_ROWS   one wavefront per body, 4 KiB rows
+ *   RPCCRC_RAGGED_PACKED 1 KiB chunks of consecutive bodies packed four per
+ *                        row, balanced by chunk count
+ * Returns RPCCRC_EINVAL for any other value. */
+#define RPCCRC_RAGGED_AUTO 0
+#define RPCCRC_RAGGED_ROWS 1
+#define RPCCRC_RAGGED_PACKED 2
+RPCCRC_API int rpc_crc32_set_ragged_path(int path);
 
 /* Human-readable text for a negative return code. */
 RPCCRC_API const char *rpc_crc32_strerror(int err);

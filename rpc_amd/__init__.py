@@ -37,6 +37,7 @@ __all__ = [
     "fill_random",
     "stream_read",
     "set_options",
+    "set_ragged_path",
     "device_info",
     "RPC_HEADER_LEN",
     "RPC_TYPE_DATA",
@@ -215,6 +216,17 @@ def stream_read(tensor, pattern: int = 0, nontemporal: bool = False, nbytes: Opt
 
 def set_options(nontemporal: bool = False, max_blocks: int = 0):
     check(_lib.rpc_crc32_set_options(int(nontemporal), max_blocks), "rpc_crc32_set_options")
+
+
+#: rpc_crc32_set_ragged_path codes (include/rpccrc.h RPCCRC_RAGGED_*)
+RAGGED_PATHS = {"auto": 0, "rows": 1, "packed": 2}
+
+
+def set_ragged_path(path="auto"):
+    """Kernel for ragged device batches: "auto", "rows" (one wavefront per body)
+    or "packed" (1 KiB chunks of consecutive bodies, four per row)."""
+    code = RAGGED_PATHS[path] if isinstance(path, str) else int(path)
+    check(_lib.rpc_crc32_set_ragged_path(code), "rpc_crc32_set_ragged_path")
 
 
 def device_info() -> str:

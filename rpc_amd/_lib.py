@@ -60,6 +60,7 @@ rpc_crc32_combine = _sig("rpc_crc32_combine", _u32, _u32, _u32, _u64)
 rpc_crc32_fill_random_device = _sig("rpc_crc32_fill_random_device", _i32, _vp, _u64, _u64, _vp)
 rpc_crc32_stream_read_device = _sig("rpc_crc32_stream_read_device", _i32, _vp, _u64, _i32, _i32, _vp)
 rpc_crc32_set_options = _sig("rpc_crc32_set_options", _i32, _i32, _i32)
+rpc_crc32_set_ragged_path = _sig("rpc_crc32_set_ragged_path", _i32, _i32)
 rpc_crc32_strerror = _sig("rpc_crc32_strerror", ctypes.c_char_p, _i32)
 rpc_crc32_device_info = _sig("rpc_crc32_device_info", _i32, ctypes.c_char_p, _sz)
 
@@ -78,6 +79,7 @@ EXPORTS = (
     "rpc_crc32_fill_random_device",
     "rpc_crc32_stream_read_device",
     "rpc_crc32_set_options",
+    "rpc_crc32_set_ragged_path",
     "rpc_crc32_strerror",
     "rpc_crc32_device_info",
 )

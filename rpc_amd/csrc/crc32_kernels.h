@@ -38,6 +38,26 @@ struct CombineArgs {
 // each with len + ((-(end address)) & 15) <= 1024.
 hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream);
 hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream);
+
+// Packed ragged batches (crc32_packed.h): 1 KiB chunks of consecutive bodies,
+// four per row, balanced by chunk count; n < 2^32 - 1.  ws must hold
+// packed_workspace_bytes(n, max_slices) bytes of device memory, stream-ordered
+// with the launch (count, scan, plan and CRC kernels all run on `stream`).
+struct PackedBatch {
+  const uint8_t *base;
+  const uint64_t *offsets;
+  const uint32_t *lengths;
+  uint64_t n;
+  uint32_t mode;
+  const uint4 *lds_image;
+  const uint32_t *tq;
+  uint32_t *out;
+  void *ws;
+  size_t ws_bytes;
+  uint64_t max_slices; // slice-table capacity (balance granularity)
+};
+hipError_t packed_workspace_bytes(uint64_t n, uint64_t max_slices, size_t *bytes);
+hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hipStream_t stream);
 hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream);
 hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool nt, int max_blocks, uint32_t *out,
                               hipStream_t stream);

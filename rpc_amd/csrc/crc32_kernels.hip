@@ -16,9 +16,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include "crc32_gf2.h"
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
+#include "crc32_packed.h"
 #include "crc32_rows.h"
 
 namespace rpccrc {
@@ -146,6 +149,105 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
 hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream) {
   if (a.n_bodies == 0) return hipSuccess;
   hipLaunchKernelGGL(crc32_chunk_combine_kernel, dim3((unsigned)a.n_bodies), dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Packed ragged batches (crc32_packed.h): per-body chunk counts, their
+// exclusive scan (rocPRIM), the slice plan, then the packed kernel.  All four
+// are stream-ordered; nothing here waits on the device.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr uint64_t kPackedMinSlice = 8; // chunks per slice, at least
+
+__global__ void __launch_bounds__(256) packed_count_kernel(const uint8_t *base, const uint64_t *offsets,
+                                                           const uint32_t *lengths, uint64_t n, uint32_t *cnt,
+                                                           uint32_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t len = lengths[i];
+  cnt[i] = packed::body_chunks((uint64_t)(uintptr_t)base + offsets[i] + len, len);
+  if (len == 0) out[i] = 0u; // empty bodies never enter the chunk stream (zlib: crc of nothing = 0)
+}
+
+// Thread i = 0..n writes slice_body[s] = i for every slice whose first chunk
+// s*S lies in (cfirst[i-1], cfirst[i]] (thread n, the sentinel, up to nslices).
+__global__ void __launch_bounds__(256) packed_plan_kernel(const uint64_t *cfirst, const uint32_t *cnt, uint64_t n,
+                                                          uint64_t max_slices, uint32_t *slice_body, uint64_t *plan) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i > n) return;
+  const uint64_t total = cfirst[n - 1] + cnt[n - 1];
+  uint64_t S = (total + max_slices - 1) / max_slices;
+  if (S < kPackedMinSlice) S = kPackedMinSlice;
+  const uint64_t nslices = (total + S - 1) / S;
+  if (i == 0) {
+    plan[0] = nslices;
+    plan[1] = S;
+  }
+  const uint64_t s_lo = (i == 0) ? 0 : cfirst[i - 1] / S + 1;
+  uint64_t s_hi = (i < n) ? cfirst[i] / S : nslices;
+  if (s_hi > nslices) s_hi = nslices;
+  for (uint64_t s = s_lo; s <= s_hi; ++s) slice_body[s] = (uint32_t)i;
+}
+
+constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+hipError_t packed_scan(void *tmp, size_t &bytes, const uint32_t *cnt, uint64_t *cfirst, uint64_t n, hipStream_t s) {
+  return rocprim::exclusive_scan(tmp, bytes, cnt, cfirst, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s);
+}
+} // namespace
+
+hipError_t packed_workspace_bytes(uint64_t n, uint64_t max_slices, size_t *bytes) {
+  size_t scan = 0;
+  const hipError_t e = packed_scan(nullptr, scan, nullptr, nullptr, n, nullptr);
+  if (e != hipSuccess) return e;
+  *bytes = align256(n * 4) + align256(n * 8) + align256((max_slices + 1) * 4) + align256(16) + align256(scan);
+  return hipSuccess;
+}
+
+hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hipStream_t s) {
+  if (p.n == 0) return hipSuccess;
+  if (p.n >= 0xFFFFFFFFull || p.max_slices == 0) return hipErrorInvalidValue;
+  uint8_t *w = static_cast<uint8_t *>(p.ws);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(w);
+  w += align256(p.n * 4);
+  uint64_t *cfirst = reinterpret_cast<uint64_t *>(w);
+  w += align256(p.n * 8);
+  uint32_t *slices = reinterpret_cast<uint32_t *>(w);
+  w += align256((p.max_slices + 1) * 4);
+  uint64_t *plan = reinterpret_cast<uint64_t *>(w);
+  w += align256(16);
+  const size_t used = (size_t)(w - static_cast<uint8_t *>(p.ws));
+  if (used > p.ws_bytes) return hipErrorInvalidValue;
+  size_t scan = p.ws_bytes - used;
+  hipLaunchKernelGGL(packed_count_kernel, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p.base, p.offsets,
+                     p.lengths, p.n, cnt, p.out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = packed_scan(w, scan, cnt, cfirst, p.n, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(packed_plan_kernel, dim3((unsigned)((p.n + 1 + 255) / 256)), dim3(256), 0, s, cfirst, cnt, p.n,
+                     p.max_slices, slices, plan);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  PackedArgs a;
+  a.base = p.base;
+  a.offsets = p.offsets;
+  a.lengths = p.lengths;
+  a.n_items = p.n;
+  a.slice_body = slices;
+  a.plan = plan;
+  a.mode = p.mode;
+  a.lds_image = p.lds_image;
+  a.tq = p.tq;
+  a.out = p.out;
+  // One 1024-thread workgroup per CU; waves beyond the slice count exit at once.
+  uint64_t blocks = (p.max_slices + 15) / 16;
+  if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
+  if (nt)
+    hipLaunchKernelGGL((crc32_packed_kernel<true>), dim3((unsigned)blocks), dim3(1024), 0, s, a);
+  else
+    hipLaunchKernelGGL((crc32_packed_kernel<false>), dim3((unsigned)blocks), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

@@ -180,6 +180,25 @@ __device__ __forceinline__ uint32_t seg_crc(const uint8_t *lds, const u32x4 (&p)
   return slice4(lds, x, lsel);
 }
 
+// Workgroup copy of the kBytes LDS table image (1024 threads): all of a
+// thread's global loads in flight at once, then the LDS stores.  Whole
+// iterations and the one partial iteration are separate so that every value
+// stays in a register (a conditionally written local array went to scratch:
+// 176 B per lane, the image loaded twice).
+template <uint32_t kBytes>
+__device__ __forceinline__ void copy_lds_image(const uint4 *src, uint4 *dst) {
+  constexpr uint32_t kN16 = kBytes / 16, kFull = kN16 / 1024, kRem = kN16 % 1024;
+  const uint32_t tid = threadIdx.x;
+  uint4 t[kFull];
+#pragma unroll
+  for (uint32_t i = 0; i < kFull; ++i) t[i] = src[tid + i * 1024u];
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (kRem != 0 && tid < kRem) r = src[kFull * 1024u + tid];
+#pragma unroll
+  for (uint32_t i = 0; i < kFull; ++i) dst[tid + i * 1024u] = t[i];
+  if (kRem != 0 && tid < kRem) dst[kFull * 1024u + tid] = r;
+}
+
 // Read-only kernel inputs through the constant address space: uniform indices
 // then compile to scalar loads (s_load, counted by lgkmcnt) instead of vector
 // loads that would sit in the vmcnt queue in front of the row prefetch.
@@ -252,6 +271,11 @@ constexpr int kRowsAblNoStore = 16;     // results never stored (timing / codege
 constexpr int kRowsAblNoTranspose = 32; // skip the permlane transposes (timing only)
 constexpr int kRowsAblLdsSeed = 64;     // QB = 1 seeds from LDS TQ16 (+ ZI) instead of scalar loads (exact)
 constexpr int kRowsAblNoFastLoad = 128; // always the per-lane address path (exact)
+constexpr int kRowsAblNoImage = 256;    // no LDS image copy (timing only; with NoCompute|NoMerge)
+// Per-wave timeline (exact results): s_memrealtime (100 MHz) at entry, after
+// the LDS image, and at exit, stored by lane 0 at times[4*gw + 0..2] together
+// with the wave's task count; times = a.offsets (unused by uniform batches).
+constexpr int kRowsAblTimes = 512;
 
 namespace rows {
 
@@ -315,25 +339,14 @@ template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1>
 __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
-  {
-    const uint4 *src = a.lds_image;
-    uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
-    // All of this thread's image loads in flight at once (a rolled loop would
-    // pay one L2 round trip per 16 KiB before the first HBM byte is read).
-    constexpr uint32_t kImg16 = kLdsBytesV2 / 16, kPer = (kImg16 + 1023) / 1024;
-    uint4 t[kPer];
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      const uint32_t k = threadIdx.x + i * 1024u;
-      if (k < kImg16) t[i] = src[k];
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      const uint32_t k = threadIdx.x + i * 1024u;
-      if (k < kImg16) dst[k] = t[i];
-    }
-  }
+  uint64_t t_entry = 0, t_image = 0;
+  if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
+  // All of this thread's image loads in flight at once (a rolled loop would
+  // pay one L2 round trip per 16 KiB before the first HBM byte is read).
+  if constexpr ((ABL & kRowsAblNoImage) == 0)
+    copy_lds_image<kLdsBytesV2>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
   __syncthreads();
+  if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();
   const uint8_t *lds = reinterpret_cast<const uint8_t *>(s_lds);
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -564,6 +577,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     flush();
     if constexpr ((ABL & kRowsAblNoStore) != 0)
       if (sink == 0x9E3779B9u) a.out[gw] = sink; // keeps the results live
+    if constexpr ((ABL & kRowsAblTimes) != 0) {
+      uint64_t *times = const_cast<uint64_t *>(a.offsets);
+      const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) {
+        times[4 * gw + 0] = t_entry;
+        times[4 * gw + 1] = t_image;
+        times[4 * gw + 2] = t_exit;
+        times[4 * gw + 3] = j0;
+      }
+    }
   } else {
     // QB = 4: group g = items [4g, 4g+4), quarter b <-> item 4g+b (len + pad <= 1 KiB).
     const uint64_t ngroups = (n + 3) / 4;
@@ -698,6 +721,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     }
     flush();
+    if constexpr ((ABL & kRowsAblTimes) != 0) {
+      uint64_t *times = const_cast<uint64_t *>(a.offsets);
+      const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) {
+        times[4 * gw + 0] = t_entry;
+        times[4 * gw + 1] = t_image;
+        times[4 * gw + 2] = t_exit;
+        times[4 * gw + 3] = j0;
+      }
+    }
   }
 }
 

@@ -44,6 +44,9 @@ std::once_flag g_once[kMaxDevices];
 
 int g_nontemporal = 1; // streamed once: non-temporal loads (measured faster)
 int g_max_blocks = 0;
+int g_ragged_path = RPCCRC_RAGGED_AUTO;
+constexpr uint64_t kPackedMinBodies = 64;         // fewer bodies: one wave per body (rows kernel)
+constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
 
 int map_hip(hipError_t e) {
   if (e == hipSuccess) return RPCCRC_OK;
@@ -132,6 +135,36 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   a.tq = c.tq;
   a.out = out;
   return map_hip(launch_rows(a, QB, g_nontemporal != 0, max_blocks_for(c), s));
+}
+
+// A ragged batch on the device: the packed kernel (crc32_packed.h) for many
+// bodies, the rows kernel (one wave per body) for a few.
+int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+           uint32_t mode, uint32_t *out, hipStream_t s) {
+  const bool fits = n < 0xFFFFFFFFull;
+  const bool packed = fits && (g_ragged_path == RPCCRC_RAGGED_PACKED ||
+                               (g_ragged_path == RPCCRC_RAGGED_AUTO && n >= kPackedMinBodies));
+  if (!packed) return items(c, base, offsets, lengths, n, 0, 0, mode, out, 1, s);
+  const uint64_t ms = std::min<uint64_t>(kPackedMaxSlices, std::max<uint64_t>(8192, 4 * n));
+  size_t bytes = 0;
+  RPCCRC_TRY(packed_workspace_bytes(n, ms, &bytes));
+  void *ws = nullptr;
+  RPCCRC_TRY(hipMallocAsync(&ws, bytes, s));
+  PackedBatch p;
+  p.base = base;
+  p.offsets = offsets;
+  p.lengths = lengths;
+  p.n = n;
+  p.mode = mode;
+  p.lds_image = c.img;
+  p.tq = c.tq;
+  p.out = out;
+  p.ws = ws;
+  p.ws_bytes = bytes;
+  p.max_slices = ms;
+  const int r = map_hip(launch_packed_batch(p, g_nontemporal != 0, max_blocks_for(c), s));
+  (void)hipFreeAsync(ws, s);
+  return r;
 }
 
 // ---- large bodies: chunk expansion + combine --------------------------------
@@ -419,7 +452,7 @@ int host_batch(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets,
     if (hi > lo) RPCCRC_TRY(hipMemcpyAsync(s.dbuf, base + lo, hi - lo, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.doff, s.hoff, cnt * 8, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.dlen, s.hlen, cnt * 4, hipMemcpyHostToDevice, s.stream));
-    rc = items(c, s.dbuf, s.doff, s.dlen, cnt, 0, 0, kModeFinal, s.dout, 1, s.stream);
+    rc = ragged(c, s.dbuf, s.doff, s.dlen, cnt, kModeFinal, s.dout, s.stream);
     if (rc) return rc;
     RPCCRC_TRY(hipMemcpyAsync(s.hout, s.dout, cnt * 4, hipMemcpyDeviceToHost, s.stream));
     s.first = i;
@@ -486,8 +519,7 @@ int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, con
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) return rc;
-  return items(*c, d_base, d_offsets, d_lengths, n, 0, 0, kModeFinal, d_out, 1,
-               static_cast<hipStream_t>(stream));
+  return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream));
 }
 
 int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_len, uint64_t stride, uint32_t *d_out,
@@ -531,7 +563,7 @@ int rpc_frames_verify_device(const uint8_t *d_stream, const uint64_t *d_frame_of
   uint32_t *bexp = blen + n;
   uint32_t *bcrc = d_crc ? d_crc : bexp + n;
   rc = map_hip(launch_frames_parse(d_stream, d_frame_offsets, n, boff, blen, bexp, s));
-  if (rc == RPCCRC_OK) rc = items(*c, d_stream, boff, blen, n, 0, 0, kModeFinal, bcrc, 1, s);
+  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s);
   if (rc == RPCCRC_OK) rc = map_hip(launch_frames_compare(bcrc, bexp, n, d_ok, s));
   (void)hipFreeAsync(ws, s);
   return rc;
@@ -550,7 +582,7 @@ int rpc_frames_stamp_device(uint8_t *d_stream, const uint64_t *d_frame_offsets, 
   uint64_t *boff = reinterpret_cast<uint64_t *>(ws);
   uint32_t *bcrc = reinterpret_cast<uint32_t *>(boff + n);
   rc = map_hip(launch_frames_body_offsets(d_frame_offsets, n, boff, s));
-  if (rc == RPCCRC_OK) rc = items(*c, d_stream, boff, d_body_lens, n, 0, 0, kModeFinal, bcrc, 1, s);
+  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, d_body_lens, n, kModeFinal, bcrc, s);
   if (rc == RPCCRC_OK)
     rc = map_hip(launch_frames_stamp(d_stream, d_frame_offsets, d_body_lens, bcrc, n, version, type, s));
   (void)hipFreeAsync(ws, s);
@@ -578,6 +610,12 @@ int rpc_crc32_set_options(int nontemporal, int max_blocks) {
   if (max_blocks < 0) return RPCCRC_EINVAL;
   g_nontemporal = nontemporal ? 1 : 0;
   g_max_blocks = max_blocks;
+  return RPCCRC_OK;
+}
+
+int rpc_crc32_set_ragged_path(int path) {
+  if (path != RPCCRC_RAGGED_AUTO && path != RPCCRC_RAGGED_ROWS && path != RPCCRC_RAGGED_PACKED) return RPCCRC_EINVAL;
+  g_ragged_path = path;
   return RPCCRC_OK;
 }
 

@@ -8,6 +8,8 @@
 //
 // stdin:  QB misalign n  then n lengths; bodies are splitmix bytes (seed 7)
 //         back to back from byte `misalign` of a 16-aligned buffer.
+//         QB = 2 is the packed ragged kernel (crc32_packed.h) and reads
+//         "nwaves min_slice max_slices" after n.
 // stdout: one CRC (hex) per body.
 #include "../../rpc_amd/csrc/crc32_gf2.h"
 #include "../../rpc_amd/csrc/crc32_layout.h"
@@ -242,10 +244,184 @@ static void emu_qb4(const uint8_t *const p0[4], const uint32_t len[4], int nvali
   }
 }
 
+// ---- packed ragged kernel (crc32_packed.h) ------------------------------------
+// The plan (chunk counts, exclusive scan, slice table), every wave's scalar
+// cursor over its slices, rows of four 1 KiB chunks, the distributed run shift
+// (ST2 / RW), the scalar run XOR and the distributed ZI step of finished bodies.
+// Checks that every slice is planned once and every body is written once.
+
+static uint32_t pk_body_chunks(uint64_t end, uint32_t len) {
+  const uint32_t z = (uint32_t)(0u - (uint32_t)end) & 15u;
+  return len ? (uint32_t)(((uint64_t)len + z + 1023) / 1024) : 0u;
+}
+
+struct PkQuarter {
+  uint32_t clen = 0, z = 0, body = 0, seed = 0;
+  bool first = false, last = false, valid = false;
+  const uint8_t *p = nullptr;
+};
+
+static void emu_packed(const std::vector<const uint8_t *> &ptr, const std::vector<uint32_t> &lens, uint64_t nwaves,
+                       uint64_t min_slice, uint64_t max_slices, std::vector<uint32_t> &out) {
+  const uint64_t n = lens.size();
+  std::vector<uint32_t> cnt(n);
+  std::vector<uint64_t> cfirst(n);
+  std::vector<int> written(n, 0);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) { // packed_count_kernel + exclusive scan
+    cnt[i] = pk_body_chunks((uint64_t)(uintptr_t)ptr[i] + lens[i], lens[i]);
+    cfirst[i] = total;
+    total += cnt[i];
+    if (lens[i] == 0) {
+      out[i] = 0;
+      written[i] = 1;
+    }
+  }
+  uint64_t S = (total + max_slices - 1) / max_slices;
+  if (S < min_slice) S = min_slice;
+  const uint64_t nslices = (total + S - 1) / S;
+  std::vector<uint32_t> sb(nslices + 1, 0xFFFFFFFFu);
+  for (uint64_t i = 0; i <= n; ++i) { // packed_plan_kernel, thread i
+    const uint64_t s_lo = i == 0 ? 0 : cfirst[i - 1] / S + 1;
+    uint64_t s_hi = i < n ? cfirst[i] / S : nslices;
+    if (s_hi > nslices) s_hi = nslices;
+    for (uint64_t s = s_lo; s <= s_hi; ++s) {
+      if (sb[s] != 0xFFFFFFFFu) { fprintf(stderr, "slice %llu planned twice\n", (unsigned long long)s); exit(5); }
+      sb[s] = (uint32_t)i;
+    }
+  }
+  for (uint64_t s = 0; s <= nslices; ++s)
+    if (sb[s] == 0xFFFFFFFFu) { fprintf(stderr, "slice %llu unplanned\n", (unsigned long long)s); exit(5); }
+
+  for (uint64_t gw = 0; gw < nwaves && gw < nslices; ++gw) {
+    uint64_t s = gw;
+    uint32_t b = sb[gw] - 1u, bend = sb[gw + 1], k = 0, nch = 0, len = 0, z = 0;
+    const uint8_t *p0 = nullptr;
+    bool done = false;
+    auto settle = [&]() -> bool {
+      if (done) return false;
+      while (k >= nch) {
+        ++b;
+        while (b >= bend) {
+          s += nwaves;
+          if (s >= nslices) {
+            done = true;
+            return false;
+          }
+          b = sb[s];
+          bend = sb[s + 1];
+        }
+        len = lens[b];
+        p0 = ptr[b];
+        z = (uint32_t)(0u - (uint32_t)((uintptr_t)p0 + len)) & 15u;
+        nch = pk_body_chunks((uint64_t)(uintptr_t)p0 + len, len);
+        k = 0;
+      }
+      return true;
+    };
+    if (!settle()) continue;
+    uint32_t W = 0;
+    for (;;) {
+      PkQuarter q[4];
+      for (int bq = 0; bq < 4; ++bq) {
+        if (!settle()) continue;
+        const uint64_t v = (uint64_t)len + z;
+        const uint8_t *wend = p0 + v - (uint64_t)(nch - 1 - k) * 1024;
+        const bool first = k == 0, last = k + 1 == nch;
+        const uint8_t *rs = first ? p0 : wend - 1024;
+        const uint8_t *re = last ? p0 + len : wend;
+        q[bq].clen = (uint32_t)(re - rs);
+        q[bq].z = last ? z : 0;
+        q[bq].first = first;
+        q[bq].last = last;
+        q[bq].valid = true;
+        q[bq].body = b;
+        q[bq].seed = first ? g_tq[q[bq].clen + q[bq].z] : 0;
+        q[bq].p = rs;
+        ++k;
+      }
+      if (!q[0].valid) break;
+      static Piece P[4][64];
+      for (int bq = 0; bq < 4; ++bq) {
+        const int64_t vstart = (int64_t)q[bq].clen + q[bq].z - 1024;
+        for (int L = 0; L < 64; ++L) {
+          const int64_t v = vstart + 16 * (int64_t)piece_of_lane((uint32_t)L);
+          P[bq][L] = (q[bq].valid && q[bq].clen && v + 16 > 0) ? load_piece(q[bq].p + v) : Piece{{0, 0, 0, 0}};
+          if (vstart < 0 || q[bq].z) mask_piece(P[bq][L], v, q[bq].clen);
+        }
+      }
+      Wave sv;
+      row_chain(P, sv);
+      merge_lo(sv);
+      for (int h = 0; h < 4; ++h)
+        for (int l = 16 * h; l < 16 * h + 16; ++l)
+          if (sv[l] != sv[16 * h]) { fprintf(stderr, "row not uniform\n"); exit(4); }
+      bool endq[4], lastq[4];
+      for (int bq = 0; bq < 4; ++bq) {
+        lastq[bq] = q[bq].valid && q[bq].last;
+        endq[bq] = bq == 3 || !q[bq].valid || q[bq].last;
+      }
+      uint32_t e[4];
+      e[3] = 3;
+      e[2] = endq[2] ? 2 : 3;
+      e[1] = endq[1] ? 1 : e[2];
+      e[0] = endq[0] ? 0 : e[1];
+      const bool cont = q[0].valid && !q[0].first;
+      Wave t;
+      for (int l = 0; l < 64; ++l) {
+        const uint32_t lo = l & 15, hi = l >> 4, n8 = lo & 7;
+        const bool own = lo < 8, wl = hi == 0 && lo >= 8;
+        const uint32_t v = sv[l] ^ q[hi].seed;
+        const uint32_t nib = ((own ? v : W) >> (4 * n8)) & 15u;
+        const uint32_t d = e[hi] - hi;
+        const uint32_t a_w = !cont ? kLdsZero
+                             : (e[0] == 3 ? kLdsRW2 + n8 * 64 + nib * 4 : kLdsST2 + n8 * 256 + (2 - e[0]) * 4 + nib * 16);
+        const uint32_t a_own = kLdsST2 + n8 * 256 + (3 - d) * 4 + nib * 16;
+        t[l] = ld(own ? a_own : (wl ? a_w : kLdsZero));
+      }
+      dist_reduce8(t);
+      uint32_t acc = cont ? t[12] : 0, fin[4] = {0, 0, 0, 0};
+      for (int bq = 0; bq < 4; ++bq) {
+        acc ^= t[16 * bq + 4];
+        fin[bq] = acc;
+        if (endq[bq]) {
+          if (bq == 3 && !lastq[3]) W = acc;
+          acc = 0;
+        }
+      }
+      bool zrow[4], any = false;
+      for (int bq = 0; bq < 4; ++bq) {
+        zrow[bq] = lastq[bq] && q[bq].z;
+        any = any || zrow[bq];
+      }
+      if (any) {
+        Wave tz;
+        for (int l = 0; l < 64; ++l) {
+          const uint32_t lo = l & 15, hi = l >> 4, n8 = lo & 7;
+          const uint32_t nib = (fin[hi] >> (4 * n8)) & 15u;
+          tz[l] = ld((lo < 8 && zrow[hi]) ? kLdsZI2 + (q[hi].z - 1) * 512 + n8 * 64 + nib * 4 : kLdsZero);
+        }
+        dist_reduce8(tz);
+        for (int bq = 0; bq < 4; ++bq)
+          if (zrow[bq]) fin[bq] = tz[16 * bq + 4];
+      }
+      for (int bq = 0; bq < 4; ++bq)
+        if (lastq[bq]) {
+          if (written[q[bq].body]++) { fprintf(stderr, "body %u written twice\n", q[bq].body); exit(6); }
+          out[q[bq].body] = ~fin[bq];
+        }
+    }
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (!written[i]) { fprintf(stderr, "body %llu never written\n", (unsigned long long)i); exit(7); }
+}
+
 int main() {
   int QB, mis;
   unsigned long n;
+  unsigned long long pk_nwaves = 1, pk_min_slice = 8, pk_max_slices = 1 << 20;
   if (scanf("%d %d %lu", &QB, &mis, &n) != 3) return 1;
+  if (QB == 2 && scanf("%llu %llu %llu", &pk_nwaves, &pk_min_slice, &pk_max_slices) != 3) return 1;
   std::vector<uint32_t> lens(n);
   uint64_t total = 0;
   for (unsigned long i = 0; i < n; ++i) {
@@ -277,6 +453,10 @@ int main() {
   }
   if (QB == 1) {
     for (unsigned long i = 0; i < n; ++i) printf("%08x\n", emu_qb1(ptr[i], lens[i]));
+  } else if (QB == 2) { // packed ragged kernel
+    std::vector<uint32_t> out(n);
+    emu_packed(ptr, lens, pk_nwaves, pk_min_slice, pk_max_slices, out);
+    for (unsigned long i = 0; i < n; ++i) printf("%08x\n", out[i]);
   } else {
     for (unsigned long g = 0; g < n; g += 4) {
       int nv = (int)((n - g) < 4 ? n - g : 4);

@@ -108,27 +108,98 @@ def test_device_uniform(body_len, pad):
     assert np.array_equal(got, oracle.crc32_uniform(host, n, body_len, stride))
 
 
+@pytest.fixture(params=["rows", "packed"])
+def ragged_path(request):
+    """Both ragged-batch kernels: one wavefront per body, and 1 KiB chunks packed four per row."""
+    rpc_amd.set_ragged_path(request.param)
+    yield request.param
+    rpc_amd.set_ragged_path("auto")
+
+
+def _ragged_check(host, offs, lens):
+    got = u32(rpc_amd.device_batch(to_dev(host), to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    want = oracle.crc32_batch(host, offs, lens)
+    if not np.array_equal(got, want):
+        bad = int(np.flatnonzero(got != want)[0])
+        raise AssertionError(f"body {bad} (len {int(lens[bad])}, off {int(offs[bad])}): "
+                             f"{got[bad]:08x} != {want[bad]:08x}")
+
+
+def _packed_offsets(lens, misalign):
+    return (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]) + misalign).astype(np.uint64)
+
+
 @pytest.mark.parametrize("misalign", [0, 1, 3, 8, 13])
-def test_device_batch_ragged(misalign):
+def test_device_batch_ragged(misalign, ragged_path):
     rng = np.random.default_rng(100 + misalign)
     lens = rng.integers(0, 70000, 600).astype(np.uint32)
     lens[::37] = 0
     lens[5] = 1
     lens[6] = 65536
-    offs = (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]) + misalign).astype(np.uint64)
+    offs = _packed_offsets(lens, misalign)
     host = oracle.splitmix_bytes(int(lens.sum()) + misalign + 16, 77 + misalign)
-    got = u32(rpc_amd.device_batch(to_dev(host), to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
-    assert np.array_equal(got, oracle.crc32_batch(host, offs, lens))
+    _ragged_check(host, offs, lens)
 
 
-def test_device_batch_unordered_overlapping():
+def test_device_batch_unordered_overlapping(ragged_path):
     """Offsets in any order, bodies may overlap (each is an independent view)."""
     rng = np.random.default_rng(9)
     host = oracle.splitmix_bytes(1 << 20, 5)
     lens = rng.integers(0, 20000, 500).astype(np.uint32)
     offs = rng.integers(0, (1 << 20) - 20000, 500).astype(np.uint64)
-    got = u32(rpc_amd.device_batch(to_dev(host), to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
-    assert np.array_equal(got, oracle.crc32_batch(host, offs, lens))
+    _ragged_check(host, offs, lens)
+
+
+@pytest.mark.parametrize("misalign", [0, 5])
+def test_device_batch_tiny_bodies(misalign, ragged_path):
+    """Up to four bodies per 4 KiB row in the packed kernel, every pad z = 0..15."""
+    rng = np.random.default_rng(31 + misalign)
+    lens = rng.integers(0, 90, 20000).astype(np.uint32)
+    lens[::11] = 0
+    offs = _packed_offsets(lens, misalign)
+    host = oracle.splitmix_bytes(int(lens.sum()) + misalign + 16, 8 + misalign)
+    _ragged_check(host, offs, lens)
+
+
+def test_device_batch_chunk_boundaries(ragged_path):
+    """Lengths around the 1 KiB chunk and 4 KiB row boundaries, at every misalignment."""
+    base_lens = [1008, 1009, 1016, 1023, 1024, 1025, 1040, 2047, 2048, 2049, 3071, 3072, 3073, 4095, 4096,
+                 4097, 5119, 5120, 8191, 8192, 8193]
+    lens = np.array([L for L in base_lens for _ in range(16)] * 3, dtype=np.uint32)
+    offs = np.empty(len(lens), dtype=np.uint64)
+    pos = 0
+    for i, L in enumerate(lens):
+        pos += i % 16  # every end alignment
+        offs[i] = pos
+        pos += int(L)
+    host = oracle.splitmix_bytes(pos + 16, 12)
+    _ragged_check(host, offs, lens)
+
+
+def test_device_batch_long_and_short_mix(ragged_path):
+    """Slices that start inside long bodies (the wave owning the body's first chunk
+    runs past its slice end) next to runs of tiny and empty bodies."""
+    pattern = [65536, 1, 2, 3, 70001, 0, 0, 5000, 16, 0, 262147, 7]
+    lens = np.array(pattern * 60, dtype=np.uint32)
+    offs = _packed_offsets(lens, 3)
+    host = oracle.splitmix_bytes(int(lens.sum()) + 32, 13)
+    _ragged_check(host, offs, lens)
+
+
+def test_device_batch_all_empty(ragged_path):
+    lens = np.zeros(300, dtype=np.uint32)
+    lens[150] = 1
+    offs = np.arange(300, dtype=np.uint64)
+    host = oracle.splitmix_bytes(512, 14)
+    _ragged_check(host, offs, lens)
+    lens[150] = 0
+    _ragged_check(host, offs, lens)
+
+
+def test_ragged_path_option():
+    with pytest.raises(rpc_amd.RpcCrcError):
+        rpc_amd.set_ragged_path(7)
+    rpc_amd.set_ragged_path("auto")
 
 
 def test_device_golden_random_bodies(golden):
@@ -314,11 +385,19 @@ def test_c2_ragged_loguniform_sample():
     total = int(lens.sum())
     base = torch.empty(total + 8, dtype=torch.uint8, device=DEV)
     rpc_amd.fill_random(base, 0x5EED0004)
-    got = u32(rpc_amd.device_batch(base, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    doffs, dlens = to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))
+    got = u32(rpc_amd.device_batch(base, doffs, dlens))  # auto: the packed kernel
     rng = np.random.default_rng(4)
     for i in rng.choice(n, 1500, replace=False):
         body = base[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy()
         assert got[i] == oracle.crc32(body), int(i)
+    # every body: the two ragged kernels agree
+    rpc_amd.set_ragged_path("rows")
+    try:
+        rows = u32(rpc_amd.device_batch(base, doffs, dlens))
+    finally:
+        rpc_amd.set_ragged_path("auto")
+    assert np.array_equal(got, rows)
 
 
 def test_c4_large_bodies():

@@ -66,3 +66,25 @@ def test_emulated_rows_kernel_matches_oracle(rows_emu, QB, mis):
     for L, o in zip(lens, out):
         assert int(o, 16) == oracle.crc32(data[off:off + L]), (QB, mis, L)
         off += L
+
+
+# ---- packed ragged kernel (crc32_packed.h): chunk stream, slices, runs --------------
+
+@pytest.mark.parametrize("mis", [0, 1, 7, 15])
+@pytest.mark.parametrize("nwaves,min_slice,max_slices", [(1, 8, 1 << 20), (3, 1, 1 << 20), (5, 2, 1 << 20),
+                                                         (4, 1, 7), (64, 1, 1 << 20)])
+def test_emulated_packed_kernel_matches_oracle(rows_emu, mis, nwaves, min_slice, max_slices):
+    """Every body written once with the oracle's CRC: empty bodies, bodies of 1..4 chunks
+    in every row position, bodies spanning many rows and slices, slices that start
+    inside a long body, waves with no work."""
+    rng = np.random.default_rng(mis * 131 + nwaves * 7 + min_slice)
+    lens = (LENS + [0, 0, 1, 0, 1024, 1023, 1025, 2048, 3072, 4096, 5000] + rng.integers(0, 200, 40).tolist()
+            + rng.integers(0, 9000, 12).tolist() + [0, 70000, 2, 0, 17])
+    inp = f"2 {mis} {len(lens)} {nwaves} {min_slice} {max_slices}\n" + "\n".join(map(str, lens)) + "\n"
+    out = subprocess.run([rows_emu], input=inp.encode(), capture_output=True, check=True).stdout.decode().split()
+    assert len(out) == len(lens)
+    data = oracle.splitmix_bytes(sum(lens) + mis, 7)
+    off = mis
+    for i, (L, o) in enumerate(zip(lens, out)):
+        assert int(o, 16) == oracle.crc32(data[off:off + L]), (i, mis, L)
+        off += L

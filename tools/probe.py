@@ -77,7 +77,8 @@ def ablate_variants(w, a):
               (1, 1, 1, 6, 1), (1, 1, 1, 0, 2), (1, 1, 0, 0, 2), (1, 1, 1, 3, 2),
               (1, 1, 1, 8, 1), (1, 1, 1, 11, 1), (1, 1, 1, 9, 1), (1, 1, 0, 11, 1), (1, 1, 0, 3, 1),
               (1, 1, 1, 16, 1), (1, 1, 1, 19, 1), (1, 1, 1, 32, 1), (1, 1, 1, 35, 1), (1, 1, 1, 51, 1),
-              (1, 1, 1, 64, 1), (1, 1, 1, 128, 1), (1, 1, 1, 192, 1), (1, 1, 1, 67, 1), (1, 1, 1, 131, 1), (1, 1, 1, 195, 1)]
+              (1, 1, 1, 64, 1), (1, 1, 1, 128, 1), (1, 1, 1, 192, 1), (1, 1, 1, 67, 1), (1, 1, 1, 131, 1), (1, 1, 1, 195, 1),
+              (1, 1, 1, 259, 1), (1, 1, 1, 275, 1)]
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
                    (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)]
@@ -90,11 +91,64 @@ def ablate_variants(w, a):
     torch.cuda.synchronize()
     ref = w.out.clone()
     for c in combos:
-        if c[3] & ~192 == 0:  # exact variants (seed source / load path only)
+        if c[3] & ~(192 | 512) == 0:  # exact variants (seed source / load path / timeline only)
             mk(*c)()
             torch.cuda.synchronize()
             assert torch.equal(out, ref), c
     return v
+
+
+def timeline(w, a):
+    """Per-wave entry / LDS-image-ready / exit times (s_memrealtime, 100 MHz) of the
+    product kernel (kRowsAblTimes variant, exact results) after a clock prewarm:
+    how much of a launch is fill (launch spread + image copy) and drain (exit spread)."""
+    import time
+    so = os.path.join(REPO, "tools", "libprobe.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tools")], check=True)
+    lib = ctypes.CDLL(so)
+    lib.probe_rows_times.restype = ctypes.c_int
+    lib.probe_rows_times.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                     ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+    qb = 4 if w.L <= 1024 else 1
+    nw = 256 * 16
+    times = torch.zeros(nw * 4, dtype=torch.int64, device=w.device)
+    out = torch.empty(w.n, dtype=torch.int32, device=w.device)
+    s = torch.cuda.current_stream()
+
+    def f():
+        rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1, 512, 1, 256,
+                                  s.cuda_stream, times.data_ptr())
+        assert rc == 0, rc
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        w.step()
+    torch.cuda.synchronize()
+    for rep in range(a.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        w.step()
+        e0.record(s)
+        f()
+        e1.record(s)
+        w.step()
+        torch.cuda.synchronize()
+        t = times.view(nw, 4).cpu().numpy().astype(np.float64)
+        live = t[:, 2] > 0
+        t = t[live]
+        base = t[:, 0].min()
+        ent, img, ext = (t[:, 0] - base) / 100.0, (t[:, 1] - base) / 100.0, (t[:, 2] - base) / 100.0  # us
+        pct = lambda x: [round(float(np.percentile(x, q)), 2) for q in (0, 50, 99, 100)]
+        print(json.dumps({"mode": "timeline", "config": a.config, "rep": rep, "qb": qb, "waves": int(live.sum()),
+                          "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
+                          "entry_us_p0_50_99_100": pct(ent), "image_ready_us": pct(img),
+                          "image_copy_us": pct(img - ent), "exit_us": pct(ext),
+                          "tasks_per_wave": pct(t[:, 3])}), flush=True)
+    w.step()
+    torch.cuda.synchronize()
+    ref = w.out.clone()
+    f()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), "timeline variant changed the CRCs"
 
 
 def sample_smi(stop, log):
@@ -180,7 +234,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--grids", default="0,512,1024")
-    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain"])
+    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline"])
     ap.add_argument("--launches", type=int, default=60)
     ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
@@ -189,6 +243,8 @@ def main():
     w = Workload(a.config, 0, torch.device("cuda", 0))
     if a.mode == "sustain":
         return sustain(w, a)
+    if a.mode == "timeline":
+        return timeline(w, a)
     variants = lib_variants(w, a) if a.mode == "lib" else ablate_variants(w, a)
     res = {k: [] for k in variants}
     for _ in range(a.rounds):
