@@ -200,6 +200,26 @@ def host_inclusive(w: Workload):
     return {"GiBps": round(nb * w.L / best / GiB, 2), "bytes": nb * w.L, "matches_device_path": ok}
 
 
+def rx_ring_probe():
+    """rpc.h frames (1 KiB bodies, MAX_BODY_LEN) landed in the
+    batched receive ring's pinned segments and verified on the GPU segment by
+    segment, host-inclusive (tools/rx_bench.c), next to the reference server's
+    per-frame rpc_crc32_verify (crc.c, one host core) on the same frames."""
+    import subprocess
+    exe = os.path.join(REPO, "tools", "rx_bench")
+    if not os.path.exists(exe):
+        return None
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_crc.so")
+    cmd = [exe, str(1 << 18), "1024", str(64 << 20), "3"] + ([ref] if os.path.exists(ref) else [])
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    try:
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": (p.stderr or p.stdout)[-300:], "rc": p.returncode}
+    r["rc"] = p.returncode
+    return r
+
+
 def stream_read_probe(w: Workload, reps=10):
     """Achievable HBM read rate on the same buffer: a pure streaming read with
     coalesced 16-B lanes, non-temporal (the CRC kernel's load shape) and
@@ -284,6 +304,8 @@ def main():
         extra["stream_read_probe"] = stream_read_probe(w)
         if not args.no_host_inclusive:
             extra["host_inclusive"] = host_inclusive(w)
+            if w.kind == "uniform":
+                extra["rx_ring"] = rx_ring_probe()
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(w, args.cpu_seconds)
 

@@ -48,6 +48,7 @@ extern "C" {
 #define RPCCRC_ENODEV (-19) /* no usable HIP device */
 #define RPCCRC_ENOMEM (-12) /* device or pinned allocation failed */
 #define RPCCRC_EIO (-5)     /* HIP runtime / kernel launch error */
+#define RPCCRC_EAGAIN (-11) /* receive ring: no free segment yet, poll first */
 
 /* ---- drop-in (reference crc.h) ---------------------------------------- */
 
@@ -105,6 +106,48 @@ RPCCRC_API int rpc_frames_verify_device(const uint8_t *d_stream, const uint64_t 
  * d_frame_offsets[i]; the body must already follow the header. */
 RPCCRC_API int rpc_frames_stamp_device(uint8_t *d_stream, const uint64_t *d_frame_offsets, const uint32_t *d_body_lens,
                             uint64_t n, uint16_t version, uint16_t type, void *stream);
+
+/* ---- batched server receive ring -------------------
+ * Replaces the one-frame-at-a-time verify of the reference server loop
+ * (server/rpc_server_main.c:135-238, verify at :227) for a receive loop that
+ * batches: frames from any connections are landed straight into pinned host
+ * segments (recv() into the pointer rpc_rx_ring_reserve returns, then
+ * rpc_rx_ring_commit), a full segment -- or one flushed by rpc_rx_ring_submit
+ * -- is verified on the GPU (one H2D copy, rpc_frames_verify_device, one D2H
+ * copy of the verdicts) while the next one fills, and rpc_rx_ring_poll returns
+ * the verdicts in arrival order with the caller's tag.  A ring is used by one
+ * thread; it works on the HIP device current at creation. */
+typedef struct rpc_rx_ring rpc_rx_ring_t;
+
+typedef struct {
+  uint64_t tag;         /* the caller's tag from rpc_rx_ring_commit / _push */
+  const uint8_t *frame; /* the frame (12-byte header + body) in the ring's pinned
+                           memory; valid until the next rpc_rx_ring_poll */
+  uint32_t body_len;    /* header fields, host order (rpc.h:3-8) */
+  uint16_t version;
+  uint16_t type;
+  uint32_t header_crc;  /* the crc32 the sender stamped */
+  uint32_t crc;         /* rpc_crc32 of the body, computed on the GPU */
+  uint8_t ok;           /* crc == header_crc: rpc_crc32_verify (PING/PONG: 1) */
+} rpc_rx_frame_t;
+
+/* nsegments (2..64) segments of segment_bytes bytes and max_frames frames each. */
+RPCCRC_API int rpc_rx_ring_create(rpc_rx_ring_t **ring, size_t segment_bytes, size_t max_frames, int nsegments);
+RPCCRC_API void rpc_rx_ring_destroy(rpc_rx_ring_t *ring);
+/* *dst = where to land a frame of frame_len bytes (header + body).  A segment
+ * that cannot take it is submitted first; RPCCRC_EAGAIN when every segment is
+ * still in flight or unpolled (call rpc_rx_ring_poll). */
+RPCCRC_API int rpc_rx_ring_reserve(rpc_rx_ring_t *ring, size_t frame_len, uint8_t **dst);
+/* Accepts the reserved frame; RPCCRC_EINVAL (frame dropped) unless its header
+ * body_len + 12 equals the reserved length. */
+RPCCRC_API int rpc_rx_ring_commit(rpc_rx_ring_t *ring, uint64_t tag);
+/* reserve + memcpy + commit. */
+RPCCRC_API int rpc_rx_ring_push(rpc_rx_ring_t *ring, const void *frame, size_t frame_len, uint64_t tag);
+/* Sends the partly filled segment to the GPU now (e.g. when the socket loop idles). */
+RPCCRC_API int rpc_rx_ring_submit(rpc_rx_ring_t *ring);
+/* Up to max_frames verdicts of the oldest submitted segment, in arrival order;
+ * returns their count (0 if none is ready and wait == 0) or a negative code. */
+RPCCRC_API int64_t rpc_rx_ring_poll(rpc_rx_ring_t *ring, rpc_rx_frame_t *out, size_t max_frames, int wait);
 
 /* ---- helpers ----------------------------------------------------------- */
 

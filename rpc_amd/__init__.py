@@ -19,8 +19,9 @@ from typing import Iterable, Optional, Sequence
 
 import numpy as np
 
-from . import _lib
+from . import _lib, rx_ring
 from ._lib import RpcCrcError, check, lib
+from .rx_ring import RxRing
 
 __all__ = [
     "RpcCrcError",
@@ -34,6 +35,7 @@ __all__ = [
     "device_large",
     "frames_verify",
     "frames_stamp",
+    "RxRing",
     "fill_random",
     "stream_read",
     "set_options",

@@ -56,6 +56,12 @@ rpc_frames_verify_device = _sig("rpc_frames_verify_device", _i32, _vp, _vp, _u64
 rpc_frames_stamp_device = _sig(
     "rpc_frames_stamp_device", _i32, _vp, _vp, _vp, _u64, ctypes.c_uint16, ctypes.c_uint16, _vp
 )
+rpc_rx_ring_create = _sig("rpc_rx_ring_create", _i32, ctypes.POINTER(ctypes.c_void_p), _sz, _sz, _i32)
+rpc_rx_ring_destroy = _sig("rpc_rx_ring_destroy", None, _vp)
+rpc_rx_ring_reserve = _sig("rpc_rx_ring_reserve", _i32, _vp, _sz, ctypes.POINTER(ctypes.c_void_p))
+rpc_rx_ring_commit = _sig("rpc_rx_ring_commit", _i32, _vp, _u64)
+rpc_rx_ring_push = _sig("rpc_rx_ring_push", _i32, _vp, _vp, _sz, _u64)
+rpc_rx_ring_submit = _sig("rpc_rx_ring_submit", _i32, _vp)
 rpc_crc32_combine = _sig("rpc_crc32_combine", _u32, _u32, _u32, _u64)
 rpc_crc32_fill_random_device = _sig("rpc_crc32_fill_random_device", _i32, _vp, _u64, _u64, _vp)
 rpc_crc32_stream_read_device = _sig("rpc_crc32_stream_read_device", _i32, _vp, _u64, _i32, _i32, _vp)
@@ -75,6 +81,13 @@ EXPORTS = (
     "rpc_crc32_device_large",
     "rpc_frames_verify_device",
     "rpc_frames_stamp_device",
+    "rpc_rx_ring_create",
+    "rpc_rx_ring_destroy",
+    "rpc_rx_ring_reserve",
+    "rpc_rx_ring_commit",
+    "rpc_rx_ring_push",
+    "rpc_rx_ring_submit",
+    "rpc_rx_ring_poll",
     "rpc_crc32_combine",
     "rpc_crc32_fill_random_device",
     "rpc_crc32_stream_read_device",
@@ -83,6 +96,16 @@ EXPORTS = (
     "rpc_crc32_strerror",
     "rpc_crc32_device_info",
 )
+
+
+class RxFrame(ctypes.Structure):
+    """rpc_rx_frame_t (include/rpccrc.h)."""
+    _fields_ = [("tag", ctypes.c_uint64), ("frame", ctypes.c_void_p), ("body_len", ctypes.c_uint32),
+                ("version", ctypes.c_uint16), ("type", ctypes.c_uint16), ("header_crc", ctypes.c_uint32),
+                ("crc", ctypes.c_uint32), ("ok", ctypes.c_uint8)]
+
+
+rpc_rx_ring_poll = _sig("rpc_rx_ring_poll", ctypes.c_int64, _vp, ctypes.POINTER(RxFrame), _sz, _i32)
 
 
 class RpcCrcError(RuntimeError):

@@ -22,6 +22,7 @@ struct ItemsArgs {
   const uint4 *lds_image;   // LDS table image (v2 layout, kLdsBytesV2 bytes)
   const uint32_t *tq;       // Tq[q] = A_q(0xFFFFFFFF), q = 0..4096
   uint32_t *out;            // n_items CRCs
+  uint32_t gshift;          // group dealing: each wave takes 2^gshift consecutive tasks per round
 };
 
 struct CombineArgs {

@@ -170,10 +170,12 @@ __global__ void __launch_bounds__(256) packed_count_kernel(const uint8_t *base, 
   if (len == 0) out[i] = 0u; // empty bodies never enter the chunk stream (zlib: crc of nothing = 0)
 }
 
-// Thread i = 0..n writes slice_body[s] = i for every slice whose first chunk
-// s*S lies in (cfirst[i-1], cfirst[i]] (thread n, the sentinel, up to nslices).
-__global__ void __launch_bounds__(256) packed_plan_kernel(const uint64_t *cfirst, const uint32_t *cnt, uint64_t n,
-                                                          uint64_t max_slices, uint32_t *slice_body, uint64_t *plan) {
+// Thread i = 0..n writes the record {i, lengths[i], offsets[i]} of every slice
+// whose first chunk s*S lies in (cfirst[i-1], cfirst[i]] (thread n, the
+// sentinel {n, 0, 0}, up to nslices).
+__global__ void __launch_bounds__(256) packed_plan_kernel(const uint64_t *cfirst, const uint32_t *cnt,
+                                                          const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+                                                          uint64_t max_slices, uint4 *slice_rec, uint64_t *plan) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i > n) return;
   const uint64_t total = cfirst[n - 1] + cnt[n - 1];
@@ -187,7 +189,10 @@ __global__ void __launch_bounds__(256) packed_plan_kernel(const uint64_t *cfirst
   const uint64_t s_lo = (i == 0) ? 0 : cfirst[i - 1] / S + 1;
   uint64_t s_hi = (i < n) ? cfirst[i] / S : nslices;
   if (s_hi > nslices) s_hi = nslices;
-  for (uint64_t s = s_lo; s <= s_hi; ++s) slice_body[s] = (uint32_t)i;
+  if (s_lo > s_hi) return;
+  const uint64_t off = (i < n) ? offsets[i] : 0;
+  const uint4 r = make_uint4((uint32_t)i, (i < n) ? lengths[i] : 0u, (uint32_t)off, (uint32_t)(off >> 32));
+  for (uint64_t s = s_lo; s <= s_hi; ++s) slice_rec[s] = r;
 }
 
 constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -201,7 +206,7 @@ hipError_t packed_workspace_bytes(uint64_t n, uint64_t max_slices, size_t *bytes
   size_t scan = 0;
   const hipError_t e = packed_scan(nullptr, scan, nullptr, nullptr, n, nullptr);
   if (e != hipSuccess) return e;
-  *bytes = align256(n * 4) + align256(n * 8) + align256((max_slices + 1) * 4) + align256(16) + align256(scan);
+  *bytes = align256(n * 4) + align256(n * 8) + align256((max_slices + 1) * 16) + align256(16) + align256(scan);
   return hipSuccess;
 }
 
@@ -213,8 +218,8 @@ hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hi
   w += align256(p.n * 4);
   uint64_t *cfirst = reinterpret_cast<uint64_t *>(w);
   w += align256(p.n * 8);
-  uint32_t *slices = reinterpret_cast<uint32_t *>(w);
-  w += align256((p.max_slices + 1) * 4);
+  uint4 *slices = reinterpret_cast<uint4 *>(w);
+  w += align256((p.max_slices + 1) * 16);
   uint64_t *plan = reinterpret_cast<uint64_t *>(w);
   w += align256(16);
   const size_t used = (size_t)(w - static_cast<uint8_t *>(p.ws));
@@ -226,8 +231,8 @@ hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hi
   if (e != hipSuccess) return e;
   e = packed_scan(w, scan, cnt, cfirst, p.n, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(packed_plan_kernel, dim3((unsigned)((p.n + 1 + 255) / 256)), dim3(256), 0, s, cfirst, cnt, p.n,
-                     p.max_slices, slices, plan);
+  hipLaunchKernelGGL(packed_plan_kernel, dim3((unsigned)((p.n + 1 + 255) / 256)), dim3(256), 0, s, cfirst, cnt,
+                     p.offsets, p.lengths, p.n, p.max_slices, slices, plan);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   PackedArgs a;
@@ -235,7 +240,7 @@ hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hi
   a.offsets = p.offsets;
   a.lengths = p.lengths;
   a.n_items = p.n;
-  a.slice_body = slices;
+  a.slice_rec = slices;
   a.plan = plan;
   a.mode = p.mode;
   a.lds_image = p.lds_image;

@@ -11,7 +11,7 @@
 //
 // Balance: the plan kernels (crc32_kernels.hip) split the chunk stream into
 // SLICES of S chunks; a body belongs to the slice its first chunk lies in and
-// slice_body[s] is the first body of slice s.  Slices are dealt round-robin
+// slice_rec[s] holds the first body of slice s.  Slices are dealt round-robin
 // over the waves (a moving window over HBM, like the rows kernel) and a wave
 // walks the bodies of its slices with a scalar cursor, packing chunks across
 // body and slice boundaries.  A body is always processed start to end by ONE
@@ -38,8 +38,8 @@ struct PackedArgs {
   const uint8_t *base;
   const uint64_t *offsets;    // body i = base[offsets[i], + lengths[i])
   const uint32_t *lengths;
-  uint64_t n_items;           // < 2^32 - 1 (slice_body holds u32 body indices)
-  const uint32_t *slice_body; // [nslices + 1], written by the plan kernel
+  uint64_t n_items;           // < 2^32 - 1 (slice records hold u32 body indices)
+  const uint4 *slice_rec;     // [nslices + 1] SliceRec, written by the plan kernel
   const uint64_t *plan;       // plan[0] = nslices, plan[1] = S (device-written)
   uint32_t mode;
   const uint4 *lds_image;
@@ -50,6 +50,16 @@ struct PackedArgs {
 namespace packed {
 
 constexpr uint32_t kChunk = 1024;
+
+// Plan record of slice s: its first body and that body's offset / length, so a
+// wave enters a slice with one scalar load (prefetched a slice ahead) instead
+// of a chain slice table -> body table.  Record nslices is the sentinel {n}.
+struct SliceRec {
+  uint32_t b;
+  uint32_t len;
+  uint64_t off;
+};
+static_assert(sizeof(SliceRec) == 16, "one uint4 per record");
 
 // Chunks of a body of `len` bytes ending at address `end`: windows end at the
 // virtual end end + z, z = (-end) mod 16.  Empty bodies have no chunks.
@@ -68,15 +78,22 @@ struct Quarter {
 __device__ __forceinline__ uint32_t q_clen(uint32_t i) { return i & 0x7FFu; }
 __device__ __forceinline__ uint32_t q_z(uint32_t i) { return (i >> 11) & 15u; }
 
+// The wave's scalar cursor.  Body b+1's metadata and the next slice's record
+// are loaded one step ahead, so moving to a new body or slice issues loads but
+// never waits on one in the issue path.
 struct Cursor {
-  uint64_t s;    // current slice
-  uint64_t p0;   // start address of body b
-  uint32_t b;    // current body
-  uint32_t bend; // first body of the next slice
-  uint32_t k;    // next chunk of body b
-  uint32_t nch;  // chunks of body b
+  uint64_t s;      // current slice
+  uint64_t p0;     // start address of body b
+  uint32_t b;      // current body
+  uint32_t bend;   // first body of the next slice (bodies [., bend) are ours)
+  uint32_t k;      // next chunk of body b
+  uint32_t nch;    // chunks of body b
   uint32_t len;
   uint32_t z;
+  uint64_t nb_off; // body b+1 (prefetched)
+  uint32_t nb_len;
+  SliceRec ns;     // slice s + nwaves (prefetched) and its end body
+  uint32_t ns_end;
   bool done;
 };
 
@@ -116,12 +133,31 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   const uint32_t mode = a.mode;
 
   Cursor cur;
-  auto meta = [&]() {
-    const uint64_t off = ld_const(a.offsets, cur.b);
-    cur.len = ld_const(a.lengths, cur.b);
+  const uint64_t last_body = a.n_items - 1;
+  const uint32_t *recw = reinterpret_cast<const uint32_t *>(a.slice_rec);
+  auto rec = [&](uint64_t sl) -> SliceRec { // one s_load_dwordx4
+    SliceRec x;
+    x.b = ld_const(recw, 4 * sl);
+    x.len = ld_const(recw, 4 * sl + 1);
+    x.off = (uint64_t)ld_const(recw, 4 * sl + 2) | ((uint64_t)ld_const(recw, 4 * sl + 3) << 32);
+    return x;
+  };
+  auto prefetch_body = [&]() { // body b+1 (an in-range index either way)
+    const uint64_t nb = (uint64_t)cur.b + 1 <= last_body ? (uint64_t)cur.b + 1 : last_body;
+    cur.nb_off = ld_const(a.offsets, nb);
+    cur.nb_len = ld_const(a.lengths, nb);
+  };
+  auto prefetch_slice = [&]() { // record of slice s + nwaves (clamped in range)
+    uint64_t sl = cur.s + nwaves;
+    if (sl >= nslices) sl = nslices - 1;
+    cur.ns = rec(sl);
+    cur.ns_end = ld_const(recw, 4 * (sl + 1));
+  };
+  auto enter = [&](uint64_t off, uint32_t len) { // body b with this metadata becomes current
+    cur.len = len;
     cur.p0 = (uint64_t)(uintptr_t)a.base + off;
-    cur.z = (uint32_t)(0u - (uint32_t)(cur.p0 + cur.len)) & 15u;
-    cur.nch = body_chunks(cur.p0 + cur.len, cur.len);
+    cur.z = (uint32_t)(0u - (uint32_t)(cur.p0 + len)) & 15u;
+    cur.nch = body_chunks(cur.p0 + len, len);
     cur.k = 0;
   };
   // Move the cursor onto its next chunk (next body, next slice of this wave);
@@ -129,30 +165,38 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   auto settle = [&]() -> bool {
     if (cur.done) return false;
     while (cur.k >= cur.nch) {
-      ++cur.b;
-      while (cur.b >= cur.bend) {
+      if (cur.b + 1u < cur.bend) { // next body of this slice
+        ++cur.b;
+        enter(cur.nb_off, cur.nb_len);
+        prefetch_body();
+      } else { // next slice of this wave
         cur.s += nwaves;
         if (cur.s >= nslices) {
           cur.done = true;
           return false;
         }
-        cur.b = ld_const(a.slice_body, cur.s);
-        cur.bend = ld_const(a.slice_body, cur.s + 1);
+        cur.b = cur.ns.b;
+        cur.bend = cur.ns_end;
+        if (cur.b < cur.bend) enter(cur.ns.off, cur.ns.len);
+        else cur.nch = cur.k = 0; // empty slice (inside a long body of an earlier one)
+        prefetch_body();
+        prefetch_slice();
       }
-      meta();
     }
     return true;
   };
 
-  cur.s = gw;
-  cur.b = ld_const(a.slice_body, gw) - 1u; // settle() steps onto the slice's first body
-  cur.bend = ld_const(a.slice_body, gw + 1);
-  cur.k = 0;
-  cur.nch = 0;
-  cur.len = 0;
-  cur.z = 0;
-  cur.p0 = 0;
-  cur.done = false;
+  {
+    const SliceRec r0 = rec(gw);
+    cur.s = gw;
+    cur.b = r0.b;
+    cur.bend = ld_const(recw, 4 * (gw + 1));
+    cur.done = false;
+    if (cur.b < cur.bend) enter(r0.off, r0.len);
+    else cur.nch = cur.k = 0;
+    prefetch_body();
+    prefetch_slice();
+  }
   if (!settle()) return;
   const uint64_t safe = cur.p0 & ~(uint64_t)15; // 16-B block of a byte this wave reads
 

@@ -359,10 +359,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   const DistLane dl = dist_lane(lane);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * 16u;
-  // Tasks (QB = 1: items, QB = 4: groups of 4 items) are dealt round-robin:
-  // wave gw takes gw, gw + nwaves, ...  All waves then stream one contiguous
-  // window of HBM (blocked ranges put 4096 streams 1 MiB apart in lockstep:
-  // measured 6 % slower).  gw is XCD-aware: workgroups are dispatched round-
+  // Tasks (QB = 1: items, QB = 4: groups of 4 items) are dealt round-robin in
+  // groups of G (below): all waves stream one moving window of HBM (blocked
+  // ranges put 4096 streams 1 MiB apart in lockstep: measured 6 % slower).
+  // gw is XCD-aware: workgroups are dispatched round-
   // robin over the 8 XCDs, so virtual block vb = (b % 8) * (blocks / 8) + b / 8
   // makes the 32 waves whose CRCs share a 128-B output line live on one XCD,
   // whose L2 assembles the whole line (measured: strided 4-B stores from two
@@ -373,7 +373,25 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   const uint32_t mode = a.mode;
   const uint64_t n = a.n_items;
   const uint64_t n_tasks = (QB == 4) ? (n + 3) / 4 : n;
-  if (gw >= n_tasks) return;
+  // Group dealing, G = 2^a.gshift: in each whole round of nwaves * G tasks,
+  // wave gw takes the G consecutive tasks [gw * G, gw * G + G), so its results
+  // of a round are G consecutive outputs (G = 32: the wave writes whole 128-B
+  // lines).  Tasks past the last whole round are dealt round-robin.
+  const uint32_t gshift = a.gshift;
+  const uint64_t gmask = (1ull << gshift) - 1;
+  const uint64_t tail_base = n_tasks / (nwaves << gshift) * (nwaves << gshift);
+  const uint64_t jg = tail_base / nwaves; // tasks per wave dealt in groups
+  auto task_of = [&](uint64_t j) -> uint64_t { // the wave's j-th task
+    return j < jg ? ((((j >> gshift) * nwaves + gw) << gshift) | (j & gmask)) : tail_base + gw + (j - jg) * nwaves;
+  };
+  auto next_task = [&](uint64_t t) -> uint64_t { // the wave's task after task t
+    if (t >= tail_base) return t + nwaves;
+    if (((t + 1) & gmask) != 0) return t + 1;
+    const uint64_t u = t + 1 + ((nwaves - 1) << gshift);
+    return u < tail_base ? u : tail_base + gw;
+  };
+  const uint64_t first_task = task_of(0);
+  if (first_task >= n_tasks) return;
 
   auto synth = [&](uint64_t key, u32x4 (&buf)[4]) {
 #pragma unroll
@@ -441,7 +459,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t sink = 0;
     auto flush = [&]() {
       if constexpr ((ABL & kRowsAblNoStore) == 0) {
-        if (lane < ocount) a.out[gw + (j0 + lane) * nwaves] = outv;
+        if (lane < ocount) a.out[task_of(j0 + lane)] = outv;
       } else {
         sink ^= outv;
       }
@@ -486,7 +504,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     };
 
-    uint64_t c_item = gw;
+    uint64_t c_item = first_task;
     uint64_t c_p0, c_lp;
     uint32_t c_len, c_z, c_nr, c_seed, c_r = 0;
     meta(c_item, c_p0, c_lp, c_len, c_z, c_nr, c_seed);
@@ -498,9 +516,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
                     bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr,
                     uint32_t &seed) {
       const bool adv = r + 1 < nr;
-      s_item = adv ? item : item + nwaves;
+      s_item = adv ? item : next_task(item);
       s_ok = ok && s_item < n;
-      meta(s_ok ? s_item : gw, p0, lp, len, z, snr, seed);
+      meta(s_ok ? s_item : first_task, p0, lp, len, z, snr, seed);
       s_r = adv ? r + 1 : 0u;
     };
     // The unrolled loops have ONE exit, at the bottom: a mid-body break edge
@@ -646,7 +664,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t outv = 0, ocount = 0;
     uint64_t j0 = 0;
     auto flush = [&]() {
-      const uint64_t item = 4 * (gw + (j0 + lane / 4u) * nwaves) + (lane & 3u);
+      const uint64_t item = 4 * task_of(j0 + lane / 4u) + (lane & 3u);
       if (lane < ocount && item < n) a.out[item] = outv;
       j0 += ocount / 4u;
       ocount = 0;
@@ -679,13 +697,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       ocount += 4;
       if (ocount == 64u) flush();
     };
-    uint64_t g = gw;
+    uint64_t g = first_task;
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       QuadMeta c_qm = issue(g, true, safe, bufA);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
-        const uint64_t ng = g + nwaves;
+        const uint64_t ng = next_task(g);
         const bool ok = ng < ngroups;
         const QuadMeta n_qm = issue(ok ? ng : g, ok, safe, nb);
         compute(c_qm, cb);
@@ -700,18 +718,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
-      {
-        const uint64_t g1 = g + nwaves;
-        n_qm = issue(g1 < ngroups ? g1 : g, g1 < ngroups, safe, bufB);
-      }
+      uint64_t gn = next_task(g);
+      n_qm = issue(gn < ngroups ? gn : g, gn < ngroups, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
-        const uint64_t g2 = g + 2 * nwaves;
+        const uint64_t g2 = next_task(gn);
         const bool ok2 = g2 < ngroups;
         const QuadMeta m_qm = issue(ok2 ? g2 : g, ok2, safe, fb);
         compute(c_qm, cb);
         c_qm = n_qm;
         n_qm = m_qm;
-        g += nwaves;
+        g = gn;
+        gn = g2;
         return g < ngroups;
       };
       for (;;) {

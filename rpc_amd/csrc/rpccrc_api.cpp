@@ -45,6 +45,7 @@ std::once_flag g_once[kMaxDevices];
 int g_nontemporal = 1; // streamed once: non-temporal loads (measured faster)
 int g_max_blocks = 0;
 int g_ragged_path = RPCCRC_RAGGED_AUTO;
+constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kPackedMinBodies = 64;         // fewer bodies: one wave per body (rows kernel)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
 
@@ -134,6 +135,7 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   a.lds_image = c.img;
   a.tq = c.tq;
   a.out = out;
+  a.gshift = kRowsGroupShift;
   return map_hip(launch_rows(a, QB, g_nontemporal != 0, max_blocks_for(c), s));
 }
 
@@ -626,6 +628,7 @@ const char *rpc_crc32_strerror(int err) {
   case RPCCRC_ENODEV: return "no usable HIP device (gfx950 with 160 KiB LDS required)";
   case RPCCRC_ENOMEM: return "out of device or pinned memory";
   case RPCCRC_EIO: return "HIP runtime error";
+  case RPCCRC_EAGAIN: return "no free receive-ring segment (poll first)";
   default: return "unknown error";
   }
 }

@@ -25,7 +25,7 @@ run() { # name timeout cmd...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
-    tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     bench) run bench 600 python bench.py ;;
     probe) run probe 600 python tools/probe.py ;;
     ablate) run ablate 600 python tools/probe.py --mode ablate --rounds 3 ;;
@@ -34,6 +34,10 @@ for s in $STEPS; do
     ablate_c1) run ablate_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 --only qb4_pair1_nt1_abl0_d1,qb4_pair1_nt1_abl3_d1,qb4_pair1_nt1_abl4_d1,qb4_pair1_nt1_abl0_d2 ;;
     bench_c1) run bench_c1 600 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive ;;
     bench_c2) run bench_c2 600 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive ;;
+    bench_c2_rows) run bench_c2_rows 600 python bench.py --config c2 --ragged-path rows --no-cpu-baseline --no-host-inclusive ;;
+    timeline) run timeline 300 python tools/probe.py --mode timeline --reps 3 ;;
+    timeline_c1) run timeline_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 ;;
+    ablate_mem) run ablate_mem 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl19_d1,qb1_pair1_nt1_abl259_d1,qb1_pair1_nt1_abl275_d1 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \

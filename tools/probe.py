@@ -67,11 +67,11 @@ def ablate_variants(w, a):
     out = torch.empty(w.n, dtype=torch.int32, device=w.device)
     blocks = 256
 
-    def mk(qb, pair, nt, abl, depth):
-        def f():
-            rc = lib.probe_rows(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, pair, nt, abl, depth, blocks,
-                                torch.cuda.current_stream().cuda_stream)
-            assert rc == 0, (qb, pair, nt, abl, depth, rc)
+    def mk(qb, pair, nt, abl, depth, g=0):
+        def f():  # pair's high byte carries the group-dealing shift (a.gshift)
+            rc = lib.probe_rows(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, pair | (g << 8), nt, abl, depth,
+                                blocks, torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, (qb, pair, nt, abl, depth, g, rc)
         return f
     combos = [(1, 1, 1, 0, 1), (1, 1, 0, 0, 1), (1, 1, 1, 1, 1), (1, 1, 1, 2, 1), (1, 1, 1, 3, 1), (1, 1, 1, 4, 1),
               (1, 1, 1, 6, 1), (1, 1, 1, 0, 2), (1, 1, 0, 0, 2), (1, 1, 1, 3, 2),
@@ -79,13 +79,17 @@ def ablate_variants(w, a):
               (1, 1, 1, 16, 1), (1, 1, 1, 19, 1), (1, 1, 1, 32, 1), (1, 1, 1, 35, 1), (1, 1, 1, 51, 1),
               (1, 1, 1, 64, 1), (1, 1, 1, 128, 1), (1, 1, 1, 192, 1), (1, 1, 1, 67, 1), (1, 1, 1, 131, 1), (1, 1, 1, 195, 1),
               (1, 1, 1, 259, 1), (1, 1, 1, 275, 1)]
+    combos += [(1, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(1, 1, 1, 3, 1, 5), (1, 1, 1, 19, 1, 5)]
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
-                   (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)]
+                   (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)] + [(4, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)]
+
+    def name(c):
+        return "qb{}_pair{}_nt{}_abl{}_d{}".format(*c[:5]) + (f"_g{c[5]}" if len(c) > 5 and c[5] else "")
     if a.only:
         keep = set(a.only.split(","))
-        combos = [c for c in combos if "qb{}_pair{}_nt{}_abl{}_d{}".format(*c) in keep]
-    v = {"qb{}_pair{}_nt{}_abl{}_d{}".format(*c): (mk(*c), w.algo_bytes, None) for c in combos}
+        combos = [c for c in combos if name(c) in keep]
+    v = {name(c): (mk(*c), w.algo_bytes, None) for c in combos}
     # correctness of every non-ablated variant vs the product kernel
     w.step()
     torch.cuda.synchronize()
@@ -109,7 +113,8 @@ def timeline(w, a):
     lib = ctypes.CDLL(so)
     lib.probe_rows_times.restype = ctypes.c_int
     lib.probe_rows_times.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
-                                     ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+                                     ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p,
+                                                                               ctypes.c_int]
     qb = 4 if w.L <= 1024 else 1
     nw = 256 * 16
     times = torch.zeros(nw * 4, dtype=torch.int64, device=w.device)
@@ -118,7 +123,7 @@ def timeline(w, a):
 
     def f():
         rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1, 512, 1, 256,
-                                  s.cuda_stream, times.data_ptr())
+                                  s.cuda_stream, times.data_ptr(), a.gshift)
         assert rc == 0, rc
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
@@ -138,7 +143,16 @@ def timeline(w, a):
         base = t[:, 0].min()
         ent, img, ext = (t[:, 0] - base) / 100.0, (t[:, 1] - base) / 100.0, (t[:, 2] - base) / 100.0  # us
         pct = lambda x: [round(float(np.percentile(x, q)), 2) for q in (0, 50, 99, 100)]
+        # per XCD (workgroup b runs on XCD b % 8; gw = vb * 16 + wave, vb = (b % 8) * 32 + b / 8)
+        xcd = (np.arange(nw) // 16 // 32)[live]
+        per_xcd = [round(float(np.median(ext[xcd == x])), 1) for x in range(8)]
+        wiw = (np.arange(nw) % 16)[live]
+        per_wave_slot = [round(float(np.median(ext[wiw == k])), 1) for k in range(16)]
+        if a.save:
+            np.save(f"{a.save}_rep{rep}.npy", np.stack([ent, img, ext]))
         print(json.dumps({"mode": "timeline", "config": a.config, "rep": rep, "qb": qb, "waves": int(live.sum()),
+                          "gshift": a.gshift, "exit_median_per_xcd": per_xcd,
+                          "exit_median_per_wave_slot": per_wave_slot,
                           "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
                           "entry_us_p0_50_99_100": pct(ent), "image_ready_us": pct(img),
                           "image_copy_us": pct(img - ent), "exit_us": pct(ext),
@@ -238,6 +252,8 @@ def main():
     ap.add_argument("--launches", type=int, default=60)
     ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
+    ap.add_argument("--gshift", type=int, default=0, help="timeline: group-dealing shift of the rows kernel")
+    ap.add_argument("--save", default="", help="timeline: save per-wave times to <save>_rep<k>.npy")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     w = Workload(a.config, 0, torch.device("cuda", 0))

@@ -41,7 +41,8 @@ void go(const ItemsArgs &a, int blocks, hipStream_t s) {
 extern "C" __attribute__((visibility("default"))) int probe_rows_times(const uint8_t *d_base, uint64_t n,
                                                                         uint32_t len, uint64_t stride, uint32_t *d_out,
                                                                         int qb, int pair, int nt, int abl, int depth,
-                                                                        int blocks, void *stream, uint64_t *d_times) {
+                                                                        int blocks, void *stream, uint64_t *d_times,
+                                                                        int gshift) {
   if (ensure_tables()) return -12;
   ItemsArgs a;
   a.base = d_base;
@@ -54,6 +55,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_times(const uin
   a.lds_image = g_img;
   a.tq = g_tq;
   a.out = d_out;
+  a.gshift = (uint32_t)gshift;
   hipStream_t s = static_cast<hipStream_t>(stream);
   V(1, 1, 0, 1) V(1, 0, 0, 1) V(1, 1, 1, 1) V(1, 1, 2, 1) V(1, 1, 3, 1) V(1, 1, 4, 1) V(1, 1, 6, 1)
   V(1, 1, 0, 2) V(1, 0, 0, 2) V(1, 1, 3, 2) V(1, 1, 8, 1) V(1, 1, 11, 1) V(1, 1, 9, 1) V(1, 0, 11, 1) V(1, 0, 3, 1) V(1, 1, 16, 1) V(1, 1, 19, 1) V(1, 1, 32, 1) V(1, 1, 35, 1) V(1, 1, 51, 1) V(1, 1, 64, 1) V(1, 1, 128, 1) V(1, 1, 192, 1) V(1, 1, 67, 1) V(1, 1, 131, 1) V(1, 1, 195, 1)
@@ -66,5 +68,6 @@ extern "C" __attribute__((visibility("default"))) int probe_rows(const uint8_t *
                                                                   uint64_t stride, uint32_t *d_out, int qb, int pair,
                                                                   int nt, int abl, int depth, int blocks,
                                                                   void *stream) {
-  return probe_rows_times(d_base, n, len, stride, d_out, qb, pair, nt, abl, depth, blocks, stream, nullptr);
+  return probe_rows_times(d_base, n, len, stride, d_out, qb, pair, nt, abl, depth, blocks, stream, nullptr,
+                          pair >> 8);
 }

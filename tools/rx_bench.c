@@ -1,0 +1,136 @@
+// tools/rx_bench.c -- MEASUREMENT ONLY: host-inclusive batched verify of rpc.h
+// frames through librpccrc's receive ring (rpc_rx_ring_*),
+// next to what the reference server does per frame: rpc_crc32_verify of the body
+// against the header CRC (server/rpc_server_main.c:227), timed with the
+// reference's own crc.c (oracle/_ref/libref_crc.so, dlopen'ed) on one host core.
+//
+// usage: rx_bench [nframes] [body_len] [segment_bytes] [nsegments] [ref_lib]
+// prints one JSON object.
+#include <dlfcn.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "rpccrc.h"
+
+static double now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static void put_be(uint8_t *p, uint32_t v, int n) {
+  for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * (n - 1 - i)));
+}
+
+int main(int argc, char **argv) {
+  const size_t nframes = argc > 1 ? strtoull(argv[1], 0, 10) : (1u << 18);
+  const size_t body = argc > 2 ? strtoull(argv[2], 0, 10) : 1024; // MAX_BODY_LEN (rpc.h:17)
+  const size_t seg = argc > 3 ? strtoull(argv[3], 0, 10) : (64u << 20);
+  const int nseg = argc > 4 ? atoi(argv[4]) : 3;
+  const char *reflib = argc > 5 ? argv[5] : NULL;
+  const size_t flen = 12 + body;
+  uint8_t *frames = malloc(nframes * flen);
+  uint64_t *offs = malloc(nframes * 8);
+  uint32_t *lens = malloc(nframes * 4), *crc = malloc(nframes * 4);
+  if (!frames || !offs || !lens || !crc) return 2;
+  // Bodies: printable bytes (JSON-like text); headers stamped with the GPU CRC.
+  for (size_t i = 0; i < nframes; ++i) {
+    uint8_t *b = frames + i * flen + 12;
+    for (size_t k = 0; k < body; ++k) b[k] = (uint8_t)(32 + mix64(i * 1000003ull + k) % 95);
+    offs[i] = i * flen + 12;
+    lens[i] = (uint32_t)body;
+  }
+  int rc = rpc_crc32_batch(frames, offs, lens, nframes, crc, 0);
+  if (rc) {
+    fprintf(stderr, "rpc_crc32_batch: %s\n", rpc_crc32_strerror(rc));
+    return 1;
+  }
+  size_t expect_bad = 0;
+  for (size_t i = 0; i < nframes; ++i) {
+    uint8_t *h = frames + i * flen;
+    put_be(h, 1, 2);
+    put_be(h + 2, 0, 2);
+    put_be(h + 4, (uint32_t)body, 4);
+    put_be(h + 8, crc[i], 4);
+    if (i % 101 == 7) { // corrupted in transit
+      h[12 + (i % body)] ^= 0x20;
+      ++expect_bad;
+    }
+  }
+  rpc_rx_ring_t *ring = NULL;
+  const size_t max_frames = seg / flen + 1;
+  rc = rpc_rx_ring_create(&ring, seg, max_frames, nseg);
+  if (rc) {
+    fprintf(stderr, "rpc_rx_ring_create: %s\n", rpc_crc32_strerror(rc));
+    return 1;
+  }
+  rpc_rx_frame_t *res = malloc(sizeof(rpc_rx_frame_t) * max_frames);
+  double best = 1e30;
+  size_t bad = 0, got = 0, order_errors = 0;
+  for (int rep = 0; rep < 4; ++rep) {
+    bad = got = order_errors = 0;
+    const double t0 = now();
+    for (size_t i = 0; i < nframes; ++i) {
+      while ((rc = rpc_rx_ring_push(ring, frames + i * flen, flen, i)) == RPCCRC_EAGAIN) {
+        const int64_t k = rpc_rx_ring_poll(ring, res, max_frames, 1);
+        for (int64_t j = 0; j < k; ++j) {
+          bad += !res[j].ok;
+          order_errors += res[j].tag != got + (size_t)j;
+        }
+        got += (size_t)(k > 0 ? k : 0);
+      }
+      if (rc) {
+        fprintf(stderr, "push: %s\n", rpc_crc32_strerror(rc));
+        return 1;
+      }
+    }
+    rpc_rx_ring_submit(ring);
+    while (got < nframes) {
+      const int64_t k = rpc_rx_ring_poll(ring, res, max_frames, 1);
+      if (k <= 0) {
+        fprintf(stderr, "poll returned %lld with %zu of %zu frames\n", (long long)k, got, nframes);
+        return 1;
+      }
+      for (int64_t j = 0; j < k; ++j) {
+        bad += !res[j].ok;
+        order_errors += res[j].tag != got + (size_t)j;
+      }
+      got += (size_t)k;
+    }
+    const double t = now() - t0;
+    if (rep > 0 && t < best) best = t; // rep 0 warms the ring and the kernels
+  }
+  rpc_rx_ring_destroy(ring);
+  // The reference's per-frame verify (crc.c rpc_crc32 == header crc) on one core.
+  double ref_s = -1;
+  size_t ref_bad = 0;
+  if (reflib) {
+    void *h = dlopen(reflib, RTLD_NOW | RTLD_LOCAL);
+    uint32_t (*ref_crc)(const void *, size_t) = h ? (uint32_t(*)(const void *, size_t))dlsym(h, "ref_rpc_crc32") : NULL;
+    if (ref_crc) {
+      const double t0 = now();
+      for (size_t i = 0; i < nframes; ++i) {
+        const uint8_t *f = frames + i * flen;
+        const uint32_t want = ((uint32_t)f[8] << 24) | ((uint32_t)f[9] << 16) | ((uint32_t)f[10] << 8) | f[11];
+        ref_bad += ref_crc(f + 12, body) != want;
+      }
+      ref_s = now() - t0;
+    }
+  }
+  const double gib = (double)nframes * flen / (double)(1ull << 30);
+  printf("{\"frames\": %zu, \"body_len\": %zu, \"segment_bytes\": %zu, \"nsegments\": %d, "
+         "\"ring_s\": %.6f, \"ring_Mframes_per_s\": %.3f, \"ring_GiBps\": %.2f, \"bad\": %zu, \"expect_bad\": %zu, "
+         "\"order_errors\": %zu, \"ref_verify_1core_s\": %.6f, \"ref_Mframes_per_s_1core\": %.3f, \"ref_bad\": %zu}\n",
+         nframes, body, seg, nseg, best, nframes / best / 1e6, gib / best, bad, expect_bad, order_errors, ref_s,
+         ref_s > 0 ? nframes / ref_s / 1e6 : -1.0, ref_bad);
+  return (bad == expect_bad && order_errors == 0 && (ref_s < 0 || ref_bad == expect_bad)) ? 0 : 3;
+}
