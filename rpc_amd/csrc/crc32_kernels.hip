@@ -128,7 +128,16 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   const dim3 grid((unsigned)blocks), block(kWaves * 64);
   const bool ragged = a.offsets != nullptr;
   if (ragged != (a.lengths != nullptr)) return hipErrorInvalidValue;
-#define RPCCRC_ROWS(Q, N, R) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R>), grid, block, 0, stream, a)
+  // Workgroup-dynamic dealing (crc32_rows.h DYN) once every workgroup has
+  // several rounds of 32 tasks; small batches (e.g. the chunks of a few large
+  // bodies) keep the static one-task-per-wave dealing.
+  const uint64_t n_tasks = (QB == 4) ? (a.n_items + 3) / 4 : a.n_items;
+  const bool dyn = n_tasks >= 8ull * kDynRound * blocks;
+#define RPCCRC_ROWS(Q, N, R)                                                                      \
+  do {                                                                                            \
+    if (dyn) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true>), grid, block, 0, stream, a); \
+    else hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R>), grid, block, 0, stream, a);             \
+  } while (0)
   if (QB == 4) {
     if (ragged) {
       if (nt) RPCCRC_ROWS(4, true, true); else RPCCRC_ROWS(4, false, true);

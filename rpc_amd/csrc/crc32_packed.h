@@ -225,21 +225,56 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
 
   auto issue = [&](Quarter (&q)[4], u32x4 (&buf)[4]) {
     uint64_t p[4];
-    bool full = true;
+    bool full;
+    if (!cur.done && cur.k + 4u <= cur.nch) {
+      // Common case: the next four chunks all belong to the current body.
+      // Only quarter 0 can be its first chunk and only quarter 3 its last.
+      const uint64_t wend0 = cur.p0 + (uint64_t)cur.len + cur.z - (uint64_t)(cur.nch - 1u - cur.k) * kChunk;
+      const bool first = cur.k == 0, last = cur.k + 4u == cur.nch;
+      const uint32_t c0 = first ? (uint32_t)(wend0 - cur.p0) : kChunk;
+      const uint32_t c3 = last ? kChunk - cur.z : kChunk;
+      const uint32_t z3 = last ? cur.z : 0u;
+      q[0].info = c0 | (first ? kQFirst : 0u) | kQValid;
+      q[0].seed = (first && mode != kModeRaw) ? ld_const(a.tq, c0) : 0u;
+      q[1].info = kChunk | kQValid;
+      q[1].seed = 0;
+      q[2].info = kChunk | kQValid;
+      q[2].seed = 0;
+      q[3].info = c3 | (z3 << 11) | (last ? kQLast : 0u) | kQValid;
+      q[3].seed = 0;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      take(q[b], p[b]);
-      full = full && q_clen(q[b].info) == kChunk;
+      for (int b = 0; b < 4; ++b) q[b].body = cur.b;
+      p[0] = first ? cur.p0 : wend0 - kChunk;
+      p[1] = wend0;
+      p[2] = wend0 + kChunk;
+      p[3] = wend0 + 2 * kChunk;
+      cur.k += 4u;
+      full = !first && !last;
+    } else {
+      // Body or slice boundary inside the row: one chunk at a time (one copy
+      // of the cursor code; the quarter index only selects registers).
+      full = true;
+#pragma nounroll
+      for (int b = 0; b < 4; ++b) {
+        Quarter t;
+        uint64_t tp;
+        take(t, tp);
+        full = full && q_clen(t.info) == kChunk;
+        if (b == 0) { q[0] = t; p[0] = tp; }
+        else if (b == 1) { q[1] = t; p[1] = tp; }
+        else if (b == 2) { q[2] = t; p[2] = tp; }
+        else { q[3] = t; p[3] = tp; }
+      }
     }
     if (full) { // four whole 1 KiB chunks: scalar bases + the lane's constant offset
 #pragma unroll
-      for (int b = 0; b < 4; ++b) buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(p[b] + pofs));
+      for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row_rsrc(p[b]), pofs);
     } else {
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const uint32_t clen = q_clen(q[b].info);
-        const int64_t v = (int64_t)clen + (int64_t)q_z(q[b].info) - (int64_t)kChunk + (int64_t)pofs;
-        const uint64_t src = (clen != 0u && v + 16 > 0) ? p[b] + (uint64_t)v : safe;
+        const int32_t v = (int32_t)(clen + q_z(q[b].info)) - (int32_t)kChunk + (int32_t)pofs;
+        const uint64_t src = (clen != 0u && v + 16 > 0) ? p[b] + (uint64_t)(int64_t)v : safe;
         buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
       }
     }
@@ -265,8 +300,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const uint32_t clen = q_clen(q[b].info), z = q_z(q[b].info);
-      const int64_t vstart = (int64_t)clen + (int64_t)z - (int64_t)kChunk;
-      if (vstart < 0 || z != 0u) buf[b] = mask_piece(buf[b], vstart + (int64_t)pofs, clen);
+      const int32_t vstart = (int32_t)(clen + z) - (int32_t)kChunk;
+      if (vstart < 0 || z != 0u) buf[b] = mask_piece32(buf[b], vstart + (int32_t)pofs, (int32_t)clen);
       sl = (hi == (uint32_t)b) ? q[b].seed : sl;
     }
     const uint32_t v = quarter_crcs(buf) ^ sl; // row hi: q_hi (^ seed on a first chunk)

@@ -75,18 +75,20 @@ __device__ __forceinline__ uint32_t slice4w(const uint8_t *lds, uint32_t x, uint
 }
 
 
-// DPP lane moves (all lanes active, every source valid).
+// DPP lane moves (all lanes active, every source valid).  bound_ctrl is set
+// even where every source lane is valid: only then does the DPP combiner fold
+// the move into the consuming v_xor (one VALU instead of two).
 __device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) { // quad_perm [1,0,3,2]
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) { // quad_perm [2,3,0,1]
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t dpp_ror4(uint32_t v) { // row_ror:4
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t dpp_ror8(uint32_t v) { // row_ror:8
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t dpp_shr4(uint32_t v) { // row_shr:4, zeros shifted in
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true);
@@ -112,6 +114,19 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
     return *q;
 }
 
+// 16-byte load from a wave-uniform base plus a 32-bit per-lane offset, as a
+// raw buffer load: the base lives in an SGPR descriptor (2 SALU to build), the
+// lane offset in a VGPR and the quarter offset in the immediate -- no 64-bit
+// per-lane address arithmetic per row (a global_load shared with the masked
+// path was compiled with per-lane 64-bit addresses).  aux 2 = nt.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(uint64_t base) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, -1, 0x00020000);
+}
+template <bool NT>
+__device__ __forceinline__ u32x4 ldb16(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, NT ? 2 : 0);
+}
+
 // Zero bytes of a 16-byte piece (virtual offset v relative to the item start)
 // that lie before the item (pos < 0) or at/after its end (pos >= len).
 __device__ __forceinline__ u32x4 mask_piece(u32x4 x, int64_t v, int64_t len) {
@@ -121,6 +136,20 @@ __device__ __forceinline__ u32x4 mask_piece(u32x4 x, int64_t v, int64_t len) {
     uint32_t m = 0xFFFFFFFFu;
     if (lo < 0) m = (lo <= -4) ? 0u : (m << (8 * (uint32_t)(-lo)));
     const int64_t over = lo + 4 - len;
+    if (over > 0) m &= (over >= 4) ? 0u : (0xFFFFFFFFu >> (8 * (uint32_t)over));
+    x[d] &= m;
+  }
+  return x;
+}
+
+// mask_piece with 32-bit positions (|v|, len <= a few KiB: chunk windows).
+__device__ __forceinline__ u32x4 mask_piece32(u32x4 x, int32_t v, int32_t len) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int32_t lo = v + 4 * d;
+    uint32_t m = 0xFFFFFFFFu;
+    if (lo < 0) m = (lo <= -4) ? 0u : (m << (8 * (uint32_t)(-lo)));
+    const int32_t over = lo + 4 - len;
     if (over > 0) m &= (over >= 4) ? 0u : (0xFFFFFFFFu >> (8 * (uint32_t)over));
     x[d] &= m;
   }
@@ -335,10 +364,30 @@ struct QuarterInfo {
 // scalars (SGPRs); item metadata comes from scalar loads.
 // RAGGED: items come from the offsets / lengths arrays (both non-null);
 // otherwise item i is [base + i * stride, + len).
-template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1>
+// DYN (QB = 1): workgroup-dynamic dealing.  A workgroup owns ROUNDS of 32
+// consecutive tasks (round r of workgroup vb: tasks [(r * blocks + vb) * 32, +32))
+// and its 16 waves take the tasks one at a time from an LDS counter, so they
+// all finish within a task of each other.  (Static dealing leaves the waves
+// of a SIMD finishing ~10 % apart, youngest last: measured per-slot exit
+// times, tools/probe.py --mode timeline.)  Finished CRCs go to an LDS ring of
+// kDynSlots rounds; the wave completing a round stores its 32 CRCs as one
+// whole 128-B line.
+constexpr uint32_t kDynRound = 32;
+constexpr uint32_t kDynSlots = 4;
+constexpr uint32_t dyn_ctl_words(int QB) { return 1 + 2 * kDynSlots + kDynSlots * kDynRound * (uint32_t)QB; }
+
+template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool DYN = false>
 __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
+  static_assert(!DYN || DEPTH == 1, "DYN: DEPTH = 1");
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
+  // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
+  // rounds (generation), then the CRC ring (QB CRCs per task).
+  __shared__ uint32_t s_ctl[DYN ? dyn_ctl_words(QB) : 1];
+  if constexpr (DYN) {
+    if (threadIdx.x <= 2 * kDynSlots)
+      s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots : 0u;
+  }
   uint64_t t_entry = 0, t_image = 0;
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   // All of this thread's image loads in flight at once (a rolled loop would
@@ -390,7 +439,21 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     const uint64_t u = t + 1 + ((nwaves - 1) << gshift);
     return u < tail_base ? u : tail_base + gw;
   };
-  const uint64_t first_task = task_of(0);
+  // DYN: a wave's next task comes from the workgroup's LDS counter.  The
+  // atomic is issued a task ahead; its result is read at the next item switch.
+  auto dyn_grab = [&]() -> uint32_t { // lane 0 holds the grabbed index
+    uint32_t c = 0;
+    if (lane == 0) c = __hip_atomic_fetch_add(&s_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return c;
+  };
+  auto dyn_task = [&](uint64_t c) -> uint64_t { return (((c / kDynRound) * nblk + vb) * kDynRound) | (c % kDynRound); };
+  uint64_t first_c = 0, first_task;
+  if constexpr (DYN) {
+    first_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)dyn_grab());
+    first_task = dyn_task(first_c);
+  } else {
+    first_task = task_of(0);
+  }
   if (first_task >= n_tasks) return;
 
   auto synth = [&](uint64_t key, u32x4 (&buf)[4]) {
@@ -437,9 +500,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (ok && rs >= 0 && (ABL & kRowsAblNoFastLoad) == 0) {
           // Whole row inside the item: scalar row base + the lane's constant
           // piece offset + immediate quarter offsets (no per-lane address math).
-          const uint8_t *row = reinterpret_cast<const uint8_t *>(p0 + (uint64_t)rs);
+          const __amdgpu_buffer_rsrc_t row = row_rsrc(p0 + (uint64_t)rs);
 #pragma unroll
-          for (int b = 0; b < 4; ++b) buf[b] = ld16<NT>(row + pofs + b * kQuarter);
+          for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row, pofs + b * kQuarter);
         } else {
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
@@ -470,8 +533,38 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       outv = (lane == ocount) ? res : outv;
       if (++ocount == 64u) flush();
     };
+    // DYN output: CRC of the task with counter index c into the LDS ring; the
+    // wave completing a round stores the round's CRCs as one whole line.
+    auto dyn_out = [&](uint64_t c, uint32_t res) {
+      const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
+      uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots;
+      uint32_t old = 0;
+      if (lane == 0) {
+        // the slot still holds an older round that a slow wave has not finished
+        while (__hip_atomic_load(&gen[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rnd)
+          __builtin_amdgcn_s_sleep(2);
+        ring[slot * kDynRound + idx] = res;
+        old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+      const uint64_t base = ((uint64_t)rnd * nblk + vb) * kDynRound;
+      const uint32_t cnt = (n_tasks - base < kDynRound) ? (uint32_t)(n_tasks - base) : kDynRound;
+      if (old + 1u == cnt) { // this wave completed the round
+        const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
+        if constexpr ((ABL & kRowsAblNoStore) == 0) {
+          if (lane < cnt) a.out[base + lane] = v;
+        } else {
+          sink ^= v;
+        }
+        if (lane == 0) {
+          done[slot] = 0;
+          __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        j0 += cnt;
+      }
+    };
     auto compute = [&](bool valid, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
-                       u32x4 (&buf)[4]) {
+                       uint64_t cidx, u32x4 (&buf)[4]) {
       const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
       const bool last = r + 1 == nr;
       if (rs < 0 || (last && z != 0)) {
@@ -500,7 +593,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         uint32_t res = W;
         if (z != 0) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
         if (mode == kModeFinal) res = ~res;
-        if (valid) park(res);
+        if constexpr (DYN) {
+          if (valid) dyn_out(cidx, res);
+        } else {
+          if (valid) park(res);
+        }
       }
     };
 
@@ -512,11 +609,25 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // Successor of task (item, r) with metadata nr: same item next row, or the
     // wave's next item.  Invalid successors carry the wave's first item's
     // (in-range) metadata and load from `safe`; their results are dropped.
+    uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
+    if constexpr (DYN) pend = dyn_grab();
+    uint64_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
     auto succ = [&](bool ok, uint64_t item, uint32_t r, uint32_t nr, uint64_t &s_item, uint32_t &s_r,
                     bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr,
                     uint32_t &seed) {
       const bool adv = r + 1 < nr;
-      s_item = adv ? item : next_task(item);
+      if constexpr (DYN) {
+        if (adv) {
+          s_item = item;
+          m_c = c_c;
+        } else {
+          m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+          s_item = dyn_task(m_c);
+          if (ok && s_item < n) pend = dyn_grab(); // no more grabs once the wave is done
+        }
+      } else {
+        s_item = adv ? item : next_task(item);
+      }
       s_ok = ok && s_item < n;
       meta(s_ok ? s_item : first_task, p0, lp, len, z, snr, seed);
       s_r = adv ? r + 1 : 0u;
@@ -537,7 +648,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         bool m_ok;
         succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, cb);
+        c_c = m_c;
         c_ok = m_ok;
         c_seed = m_seed;
         c_item = m_item;
@@ -567,7 +679,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         bool m_ok;
         succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, cb);
         c_ok = n_ok;
         c_seed = n_seed;
         n_seed = m_seed;
@@ -647,7 +759,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       } else {
         if (full) { // four whole 1 KiB items: scalar bases, constant lane offset
 #pragma unroll
-          for (int b = 0; b < 4; ++b) buf[b] = ld16<NT>(qi[b].p0 + pofs);
+          for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row_rsrc((uint64_t)(uintptr_t)qi[b].p0), pofs);
         } else {
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
@@ -663,13 +775,43 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // Parked results: lane k = item 4 * (gw + (j0 + k / 4) * nwaves) + k % 4 (see QB = 1).
     uint32_t outv = 0, ocount = 0;
     uint64_t j0 = 0;
+    // DYN output (see QB = 1): the 4 CRCs of group task c into the LDS ring; the
+    // wave completing a round stores its (up to) 128 CRCs as two 256-B stores.
+    auto dyn_out4 = [&](uint64_t c, const uint32_t (&v)[4]) {
+      constexpr uint32_t kW = kDynRound * 4;
+      const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
+      uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots + slot * kW;
+      uint32_t old = 0;
+      if (lane == 0) {
+        while (__hip_atomic_load(&gen[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rnd)
+          __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ring[idx * 4 + b] = v[b];
+        old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
+      const uint64_t base = ((uint64_t)rnd * nblk + vb) * kDynRound; // first group of the round
+      const uint32_t cnt = (ngroups - base < kDynRound) ? (uint32_t)(ngroups - base) : kDynRound;
+      if (old + 1u == cnt) {
+        const uint64_t ibase = 4 * base;
+        const uint32_t nit = (n - ibase < kW) ? (uint32_t)(n - ibase) : kW;
+        const uint32_t v0 = ring[lane], v1 = ring[64 + lane];
+        if (lane < nit) a.out[ibase + lane] = v0;
+        if (64 + lane < nit) a.out[ibase + 64 + lane] = v1;
+        if (lane == 0) {
+          done[slot] = 0;
+          __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        j0 += cnt;
+      }
+    };
     auto flush = [&]() {
       const uint64_t item = 4 * task_of(j0 + lane / 4u) + (lane & 3u);
       if (lane < ocount && item < n) a.out[item] = outv;
       j0 += ocount / 4u;
       ocount = 0;
     };
-    auto compute = [&](const QuadMeta &qm, u32x4 (&buf)[4]) {
+    auto compute = [&](const QuadMeta &qm, uint64_t cidx, u32x4 (&buf)[4]) {
       uint32_t zl = 0, zany = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -688,27 +830,46 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         res = (zl != 0u) ? t : res; // valid in lanes 4..7 of each row
       }
       if (mode == kModeFinal) res = ~res;
+      uint32_t vals[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         uint32_t v = __builtin_amdgcn_readlane(res, 16 * b + 4);
         if ((qm.lz[b] >> 4) == 0) v = 0u;
-        outv = (lane == ocount + (uint32_t)b) ? v : outv;
+        vals[b] = v;
       }
-      ocount += 4;
-      if (ocount == 64u) flush();
+      if constexpr (DYN) {
+        dyn_out4(cidx, vals);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) outv = (lane == ocount + (uint32_t)b) ? vals[b] : outv;
+        ocount += 4;
+        if (ocount == 64u) flush();
+      }
     };
     uint64_t g = first_task;
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       QuadMeta c_qm = issue(g, true, safe, bufA);
+      uint32_t pend = 0;
+      if constexpr (DYN) pend = dyn_grab();
+      uint64_t c_c = first_c;
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
-        const uint64_t ng = next_task(g);
+        uint64_t ng, n_c = 0;
+        if constexpr (DYN) {
+          n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+          ng = dyn_task(n_c);
+        } else {
+          ng = next_task(g);
+        }
         const bool ok = ng < ngroups;
+        if constexpr (DYN)
+          if (ok) pend = dyn_grab();
         const QuadMeta n_qm = issue(ok ? ng : g, ok, safe, nb);
-        compute(c_qm, cb);
+        compute(c_qm, c_c, cb);
         c_qm = n_qm;
         g = ng;
+        c_c = n_c;
         return ok;
       };
       for (;;) {
@@ -724,7 +885,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         const uint64_t g2 = next_task(gn);
         const bool ok2 = g2 < ngroups;
         const QuadMeta m_qm = issue(ok2 ? g2 : g, ok2, safe, fb);
-        compute(c_qm, cb);
+        compute(c_qm, 0, cb);
         c_qm = n_qm;
         n_qm = m_qm;
         g = gn;

@@ -196,6 +196,31 @@ def test_device_batch_all_empty(ragged_path):
     _ragged_check(host, offs, lens)
 
 
+@pytest.mark.parametrize("n,body_len,stride", [(65536 + 12345, 1500, 1500), (262144 + 4321, 200, 203),
+                                                (65536 * 2 + 31, 4096, 4096)])
+def test_device_uniform_workgroup_dynamic(n, body_len, stride):
+    """Batches large enough for the workgroup-dynamic dealing (>= 8 rounds of 32
+    tasks per workgroup), with a partial last round and pads z != 0."""
+    host = oracle.splitmix_bytes(n * stride + 16, n ^ body_len)
+    got = u32(rpc_amd.device_uniform(to_dev(host), n, body_len, stride))
+    want = oracle.crc32_uniform(host, n, body_len, stride)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"{bad.size} mismatches, first body {int(bad[0])}"
+
+
+def test_device_batch_rows_workgroup_dynamic():
+    """The rows kernel on a large ragged batch (one wave per body, dynamic dealing)."""
+    rng = np.random.default_rng(71)
+    lens = rng.integers(0, 3000, 70001).astype(np.uint32)
+    offs = _packed_offsets(lens, 9)
+    host = oracle.splitmix_bytes(int(lens.sum()) + 32, 15)
+    rpc_amd.set_ragged_path("rows")
+    try:
+        _ragged_check(host, offs, lens)
+    finally:
+        rpc_amd.set_ragged_path("auto")
+
+
 def test_ragged_path_option():
     with pytest.raises(rpc_amd.RpcCrcError):
         rpc_amd.set_ragged_path(7)

@@ -38,6 +38,12 @@ for s in $STEPS; do
     timeline) run timeline 300 python tools/probe.py --mode timeline --reps 3 ;;
     timeline_c1) run timeline_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 ;;
     ablate_mem) run ablate_mem 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl19_d1,qb1_pair1_nt1_abl259_d1,qb1_pair1_nt1_abl275_d1 ;;
+    ablate_g) run ablate_g 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl0_d1_g1,qb1_pair1_nt1_abl0_d1_g2,qb1_pair1_nt1_abl0_d1_g3,qb1_pair1_nt1_abl0_d1_g4,qb1_pair1_nt1_abl0_d1_g5,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl3_d1_g5,qb1_pair1_nt1_abl19_d1_g5 ;;
+    ablate_g_c1) run ablate_g_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 --only qb4_pair1_nt1_abl0_d1,qb4_pair1_nt1_abl0_d1_g1,qb4_pair1_nt1_abl0_d1_g2,qb4_pair1_nt1_abl0_d1_g3,qb4_pair1_nt1_abl0_d1_g4,qb4_pair1_nt1_abl0_d1_g5 ;;
+    timeline_g5) run timeline_g5 300 python tools/probe.py --mode timeline --reps 2 --gshift 5 --save $OUT/tl_g5 ;;
+    timeline_save) run timeline_save 300 python tools/probe.py --mode timeline --reps 2 --save $OUT/tl_g0 ;;
+    ablate_dyn) run ablate_dyn 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl0_d1_g3,qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl1027_d1,qb1_pair1_nt1_abl19_d1,qb1_pair1_nt1_abl1043_d1 ;;
+    timeline_dyn) run timeline_dyn 300 python tools/probe.py --mode timeline --reps 2 --dyn --save $OUT/tl_dyn ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \

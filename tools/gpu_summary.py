@@ -32,12 +32,13 @@ for f in sorted(glob.glob(os.path.join(d, "bench*.log"))):
     cpu = j.get("cpu_baseline") or {}
     print(f"{os.path.basename(f):14s} value={j['value']:8.1f} {j['unit']} us/launch={r['avg_launch_us']:9.1f} "
           f"frac={r['frac']:.4f} traffic={r.get('traffic')} cpu={cpu.get('value')} extra={j.get('extra')}")
-for name in ("probe.log", "ablate.log", "ablate_nat.log", "ablate_c1.log", "ablate_mem.log"):
+for name in ("probe.log", "ablate.log", "ablate_nat.log", "ablate_c1.log", "ablate_mem.log", "ablate_g.log",
+             "ablate_g_c1.log", "ablate_dyn.log"):
     for l in lines(name):
         if l.startswith("{"):
             j = json.loads(l)
             print(f"{name:14s} {j['variant']:28s} {j['config']:4s} {j['median_us']:9.2f} us  {j['GBps']:8.1f} GB/s")
-for name in ("timeline.log", "timeline_c1.log"):
+for name in ("timeline.log", "timeline_c1.log", "timeline_g5.log", "timeline_save.log", "timeline_dyn.log"):
     for l in lines(name):
         if l.startswith("{"):
             print(name, l)

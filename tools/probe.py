@@ -80,9 +80,10 @@ def ablate_variants(w, a):
               (1, 1, 1, 64, 1), (1, 1, 1, 128, 1), (1, 1, 1, 192, 1), (1, 1, 1, 67, 1), (1, 1, 1, 131, 1), (1, 1, 1, 195, 1),
               (1, 1, 1, 259, 1), (1, 1, 1, 275, 1)]
     combos += [(1, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(1, 1, 1, 3, 1, 5), (1, 1, 1, 19, 1, 5)]
+    combos += [(1, 1, 1, 1024, 1), (1, 1, 1, 1027, 1), (1, 1, 1, 1043, 1)]  # DYN (+ memory only)
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
-                   (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)] + [(4, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)]
+                   (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)] + [(4, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(4, 1, 1, 1024, 1)]
 
     def name(c):
         return "qb{}_pair{}_nt{}_abl{}_d{}".format(*c[:5]) + (f"_g{c[5]}" if len(c) > 5 and c[5] else "")
@@ -95,7 +96,7 @@ def ablate_variants(w, a):
     torch.cuda.synchronize()
     ref = w.out.clone()
     for c in combos:
-        if c[3] & ~(192 | 512) == 0:  # exact variants (seed source / load path / timeline only)
+        if c[3] & ~(192 | 512 | 1024) == 0:  # exact variants (seed source / load path / timeline / DYN)
             mk(*c)()
             torch.cuda.synchronize()
             assert torch.equal(out, ref), c
@@ -122,8 +123,8 @@ def timeline(w, a):
     s = torch.cuda.current_stream()
 
     def f():
-        rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1, 512, 1, 256,
-                                  s.cuda_stream, times.data_ptr(), a.gshift)
+        rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1,
+                                  512 | (1024 if a.dyn else 0), 1, 256, s.cuda_stream, times.data_ptr(), a.gshift)
         assert rc == 0, rc
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
@@ -151,7 +152,7 @@ def timeline(w, a):
         if a.save:
             np.save(f"{a.save}_rep{rep}.npy", np.stack([ent, img, ext]))
         print(json.dumps({"mode": "timeline", "config": a.config, "rep": rep, "qb": qb, "waves": int(live.sum()),
-                          "gshift": a.gshift, "exit_median_per_xcd": per_xcd,
+                          "gshift": a.gshift, "dyn": a.dyn, "exit_median_per_xcd": per_xcd,
                           "exit_median_per_wave_slot": per_wave_slot,
                           "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
                           "entry_us_p0_50_99_100": pct(ent), "image_ready_us": pct(img),
@@ -253,6 +254,7 @@ def main():
     ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
     ap.add_argument("--gshift", type=int, default=0, help="timeline: group-dealing shift of the rows kernel")
+    ap.add_argument("--dyn", action="store_true", help="timeline: workgroup-dynamic dealing (DYN)")
     ap.add_argument("--save", default="", help="timeline: save per-wave times to <save>_rep<k>.npy")
     a = ap.parse_args()
     torch.cuda.set_device(0)

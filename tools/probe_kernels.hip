@@ -26,9 +26,15 @@ int ensure_tables() {
   return 0;
 }
 
+// abl bit 1024 (not a kernel ABL bit) selects the workgroup-dynamic dealing (DYN).
+constexpr int kProbeDyn = 1024;
 template <int QB, bool NT, int ABL, int DEPTH>
 void go(const ItemsArgs &a, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, false, ABL, DEPTH>), dim3(blocks), dim3(1024), 0, s, a);
+  if constexpr ((ABL & kProbeDyn) != 0)
+    hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, false, (ABL & ~kProbeDyn), DEPTH, true>), dim3(blocks), dim3(1024),
+                       0, s, a);
+  else
+    hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, false, ABL, DEPTH>), dim3(blocks), dim3(1024), 0, s, a);
 }
 } // namespace
 
@@ -61,6 +67,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_times(const uin
   V(1, 1, 0, 2) V(1, 0, 0, 2) V(1, 1, 3, 2) V(1, 1, 8, 1) V(1, 1, 11, 1) V(1, 1, 9, 1) V(1, 0, 11, 1) V(1, 0, 3, 1) V(1, 1, 16, 1) V(1, 1, 19, 1) V(1, 1, 32, 1) V(1, 1, 35, 1) V(1, 1, 51, 1) V(1, 1, 64, 1) V(1, 1, 128, 1) V(1, 1, 192, 1) V(1, 1, 67, 1) V(1, 1, 131, 1) V(1, 1, 195, 1)
   V(4, 1, 0, 1) V(4, 0, 0, 1) V(4, 1, 3, 1) V(4, 1, 4, 1) V(4, 1, 6, 1) V(4, 1, 0, 2) V(4, 1, 3, 2)
   V(1, 1, 259, 1) V(1, 1, 275, 1) V(1, 1, 512, 1) V(4, 1, 512, 1)
+  V(1, 1, 1024, 1) V(1, 1, 1027, 1) V(1, 1, 1043, 1) V(1, 1, 1536, 1) V(4, 1, 1024, 1) V(4, 1, 1536, 1)
   return -22;
 }
 
