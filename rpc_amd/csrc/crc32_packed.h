@@ -266,17 +266,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
         else { q[3] = t; p[3] = tp; }
       }
     }
-    if (full) { // four whole 1 KiB chunks: scalar bases + the lane's constant offset
+    (void)full;
+    // One load path for every row (a separate path for whole rows made the
+    // compiler's vmcnt accounting wait for the row just issued): the window of
+    // quarter b starts d bytes from the 16-B block holding the chunk's first
+    // byte; pieces before that block read as zeros without touching memory.
 #pragma unroll
-      for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row_rsrc(p[b]), pofs);
-    } else {
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const uint32_t clen = q_clen(q[b].info);
-        const int32_t v = (int32_t)(clen + q_z(q[b].info)) - (int32_t)kChunk + (int32_t)pofs;
-        const uint64_t src = (clen != 0u && v + 16 > 0) ? p[b] + (uint64_t)(int64_t)v : safe;
-        buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
-      }
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t clen = q_clen(q[b].info);
+      const uint64_t base = clen ? (p[b] & ~(uint64_t)15) : safe;
+      const int32_t d = clen ? (int32_t)(clen + q_z(q[b].info)) - (int32_t)kChunk + (int32_t)(p[b] & 15) : INT32_MIN / 2;
+      buf[b] = ldb16_or_zero<NT>(row_rsrc(base), d + (int32_t)pofs);
     }
   };
 

@@ -126,6 +126,13 @@ template <bool NT>
 __device__ __forceinline__ u32x4 ldb16(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, NT ? 2 : 0);
 }
+// A 16-B piece at signed offset `off` from a uniform base; pieces with off < 0
+// (before the data) are not read at all and come back as zeros: their offset
+// is replaced by one past the descriptor's range (raw buffer range check).
+template <bool NT>
+__device__ __forceinline__ u32x4 ldb16_or_zero(__amdgpu_buffer_rsrc_t rsrc, int32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, off >= 0 ? off : 0x7FFFFFF0, 0, NT ? 2 : 0);
+}
 
 // Zero bytes of a 16-byte piece (virtual offset v relative to the item start)
 // that lie before the item (pos < 0) or at/after its end (pos >= len).
@@ -497,20 +504,29 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         synth(p0 + r, buf);
       } else {
         const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
+        // One load sequence for every row (loads issued from two paths broke
+        // the compiler's vmcnt accounting: the row just issued was waited for).
+        // Whole rows: scalar row base + the lane's constant offsets.  A first
+        // row starting before the item: base = the item's first 16-B block,
+        // pieces before it read as zeros; invalid rows read nothing.
+        uint64_t base;
+        uint32_t off[4];
         if (ok && rs >= 0 && (ABL & kRowsAblNoFastLoad) == 0) {
-          // Whole row inside the item: scalar row base + the lane's constant
-          // piece offset + immediate quarter offsets (no per-lane address math).
-          const __amdgpu_buffer_rsrc_t row = row_rsrc(p0 + (uint64_t)rs);
+          base = p0 + (uint64_t)rs;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row, pofs + b * kQuarter);
+          for (int b = 0; b < 4; ++b) off[b] = pofs + b * kQuarter;
         } else {
+          base = ok ? (p0 & ~(uint64_t)15) : safe;
+          const int32_t d = ok ? (int32_t)(rs + (int64_t)(p0 & 15)) : INT32_MIN / 2;
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
-            const int64_t v = rs + b * kQuarter + (int64_t)pofs;
-            const uint64_t src = (ok && v + 16 > 0) ? p0 + (uint64_t)v : safe;
-            buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
+            const int32_t o = d + (int32_t)(pofs + b * kQuarter);
+            off[b] = o >= 0 ? (uint32_t)o : 0x7FFFFFF0u;
           }
         }
+        const __amdgpu_buffer_rsrc_t row = row_rsrc(base);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row, off[b]);
       }
     };
     uint32_t W = 0; // running crc0 (Horner over rows) of the current item, wave-uniform
@@ -757,18 +773,28 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       if constexpr ((ABL & kRowsAblNoLoad) != 0) {
         synth(g, buf);
       } else {
+        // One load sequence (see QB = 1): per quarter a uniform base (the item's
+        // first 16-B block) and per-lane offsets, zeros before the item.
+        uint64_t base[4];
+        uint32_t off[4];
         if (full) { // four whole 1 KiB items: scalar bases, constant lane offset
 #pragma unroll
-          for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row_rsrc((uint64_t)(uintptr_t)qi[b].p0), pofs);
+          for (int b = 0; b < 4; ++b) {
+            base[b] = (uint64_t)(uintptr_t)qi[b].p0;
+            off[b] = pofs;
+          }
         } else {
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
-            const int64_t v = qi[b].vstart + (int64_t)pofs;
-            const uint64_t src =
-                (ok && qi[b].len != 0 && v + 16 > 0) ? (uint64_t)(uintptr_t)qi[b].p0 + (uint64_t)v : safe;
-            buf[b] = ld16<NT>(reinterpret_cast<const uint8_t *>(src));
+            const uint64_t p = (uint64_t)(uintptr_t)qi[b].p0;
+            const bool live = ok && qi[b].len != 0;
+            base[b] = live ? (p & ~(uint64_t)15) : safe;
+            const int32_t o = live ? (int32_t)(qi[b].vstart + (int64_t)(p & 15)) + (int32_t)pofs : -1;
+            off[b] = o >= 0 ? (uint32_t)o : 0x7FFFFFF0u;
           }
         }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row_rsrc(base[b]), off[b]);
       }
       return qm;
     };

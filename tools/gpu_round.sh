@@ -44,6 +44,7 @@ for s in $STEPS; do
     timeline_save) run timeline_save 300 python tools/probe.py --mode timeline --reps 2 --save $OUT/tl_g0 ;;
     ablate_dyn) run ablate_dyn 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl0_d1_g3,qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl1027_d1,qb1_pair1_nt1_abl19_d1,qb1_pair1_nt1_abl1043_d1 ;;
     timeline_dyn) run timeline_dyn 300 python tools/probe.py --mode timeline --reps 2 --dyn --save $OUT/tl_dyn ;;
+    packed) run packed 600 python tools/probe.py --mode packed --rounds 3 --reps 5 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \

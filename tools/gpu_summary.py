@@ -42,6 +42,9 @@ for name in ("timeline.log", "timeline_c1.log", "timeline_g5.log", "timeline_sav
     for l in lines(name):
         if l.startswith("{"):
             print(name, l)
+for l in lines("packed.log"):
+    if l.startswith("{"):
+        print("packed", l)
 for l in lines("sustain.log"):
     if l.startswith('{"variant"'):
         j = json.loads(l)

@@ -166,6 +166,38 @@ def timeline(w, a):
     assert torch.equal(out, ref), "timeline variant changed the CRCs"
 
 
+def packed_modes(a):
+    """Ragged-batch kernels (rows vs packed) on shapes that isolate their costs:
+    uniform 4 KiB / 1 KiB / 3000 B bodies passed as a ragged batch, and C2."""
+    dev = torch.device("cuda", 0)
+    res = []
+    shapes = [("4096x1M", 1 << 20, 4096), ("1024x1M", 1 << 20, 1024), ("3000x1M", 1 << 20, 3000),
+              ("c2", None, None)]
+    for name, n, L in shapes:
+        if name == "c2":
+            w = Workload("c2", 0, dev)
+            base, offs, lens, nbytes = w.base, w.offs, w.lens, w.total
+        else:
+            nbytes = n * L
+            base = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+            rpc_amd.fill_random(base, 7)
+            offs = (torch.arange(n, dtype=torch.int64, device=dev) * L)
+            lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        out = torch.empty(offs.numel(), dtype=torch.int32, device=dev)
+        for path in ("rows", "packed"):
+            rpc_amd.set_ragged_path(path)
+            f = lambda: rpc_amd.device_batch(base, offs, lens, out=out)
+            ts = [timed(f, a.reps) for _ in range(a.rounds)]
+            med = statistics.median(ts)
+            r = {"mode": "packed", "shape": name, "path": path, "median_us": round(med * 1e6, 1),
+                 "GiBps": round(nbytes / med / 2**30, 1)}
+            res.append(r)
+            print(json.dumps(r), flush=True)
+        rpc_amd.set_ragged_path("auto")
+        del base, offs, lens, out
+        torch.cuda.empty_cache()
+
+
 def sample_smi(stop, log):
     """Child-process power/clock sampler (best effort; rocm-smi or amd-smi)."""
     import threading  # noqa: F401
@@ -249,7 +281,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--grids", default="0,512,1024")
-    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline"])
+    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline", "packed"])
     ap.add_argument("--launches", type=int, default=60)
     ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
@@ -258,6 +290,8 @@ def main():
     ap.add_argument("--save", default="", help="timeline: save per-wave times to <save>_rep<k>.npy")
     a = ap.parse_args()
     torch.cuda.set_device(0)
+    if a.mode == "packed":
+        return packed_modes(a)
     w = Workload(a.config, 0, torch.device("cuda", 0))
     if a.mode == "sustain":
         return sustain(w, a)
