@@ -119,8 +119,14 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
 // lane offset in a VGPR and the quarter offset in the immediate -- no 64-bit
 // per-lane address arithmetic per row (a global_load shared with the masked
 // path was compiled with per-lane 64-bit addresses).  aux 2 = nt.
+// Descriptor range: offsets >= kRsrcRange fail the raw-buffer range check and
+// read as zeros WITHOUT a memory access; kOobOffset is such an offset.  Every
+// in-range offset of the kernels is below 8 KiB.
+constexpr uint32_t kRsrcRange = 0x40000000u;
+constexpr uint32_t kOobOffset = 0x7FFFFFF0u;
+static_assert(kOobOffset >= kRsrcRange, "the out-of-range offset must fail the range check");
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(uint64_t base) {
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, -1, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)kRsrcRange, 0x00020000);
 }
 template <bool NT>
 __device__ __forceinline__ u32x4 ldb16(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
@@ -131,7 +137,7 @@ __device__ __forceinline__ u32x4 ldb16(__amdgpu_buffer_rsrc_t rsrc, uint32_t off
 // is replaced by one past the descriptor's range (raw buffer range check).
 template <bool NT>
 __device__ __forceinline__ u32x4 ldb16_or_zero(__amdgpu_buffer_rsrc_t rsrc, int32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, off >= 0 ? off : 0x7FFFFFF0, 0, NT ? 2 : 0);
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, off >= 0 ? off : (int)kOobOffset, 0, NT ? 2 : 0);
 }
 
 // Zero bytes of a 16-byte piece (virtual offset v relative to the item start)
@@ -521,7 +527,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
             const int32_t o = d + (int32_t)(pofs + b * kQuarter);
-            off[b] = o >= 0 ? (uint32_t)o : 0x7FFFFFF0u;
+            off[b] = o >= 0 ? (uint32_t)o : kOobOffset;
           }
         }
         const __amdgpu_buffer_rsrc_t row = row_rsrc(base);
@@ -790,7 +796,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
             const bool live = ok && qi[b].len != 0;
             base[b] = live ? (p & ~(uint64_t)15) : safe;
             const int32_t o = live ? (int32_t)(qi[b].vstart + (int64_t)(p & 15)) + (int32_t)pofs : -1;
-            off[b] = o >= 0 ? (uint32_t)o : 0x7FFFFFF0u;
+            off[b] = o >= 0 ? (uint32_t)o : kOobOffset;
           }
         }
 #pragma unroll

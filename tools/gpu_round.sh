@@ -20,6 +20,7 @@ run() { # name timeout cmd...
   echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
   tail -5 "$OUT/$name.log"
   if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "FATAL step $name rc=$rc; stopping"; exit $rc; fi
+  if [ "${STRICT:-0}" = 1 ] && [ $rc -ne 0 ]; then echo "STRICT: step $name failed rc=$rc; stopping"; exit $rc; fi
   return $rc
 }
 for s in $STEPS; do
