@@ -12,7 +12,8 @@
 // Balance: the plan kernels (crc32_kernels.hip) split the chunk stream into
 // SLICES of S chunks; a body belongs to the slice its first chunk lies in and
 // slice_rec[s] holds the first body of slice s.  Slices are dealt round-robin
-// over the waves (a moving window over HBM, like the rows kernel) and a wave
+// over the workgroups (a moving window over HBM, like the rows kernel), the
+// waves of a workgroup take its slices from an LDS counter, and a wave
 // walks the bodies of its slices with a scalar cursor, packing chunks across
 // body and slice boundaries.  A body is always processed start to end by ONE
 // wave (past its slice's end if need be), so the Horner chain across rows stays
@@ -92,7 +93,8 @@ struct Cursor {
   uint32_t z;
   uint64_t nb_off; // body b+1 (prefetched)
   uint32_t nb_len;
-  SliceRec ns;     // slice s + nwaves (prefetched) and its end body
+  uint64_t ns_s;   // the wave's next slice,
+  SliceRec ns;     // its record (prefetched) and its end body
   uint32_t ns_end;
   bool done;
 };
@@ -104,6 +106,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   using namespace rows;
   using namespace packed;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
+  // Workgroup-dynamic slice dealing (as the rows kernel's DYN): workgroup vb
+  // owns slices k * blocks + vb, k = 0, 1, ..., and its waves take the next k
+  // from this LDS counter, so they finish together.
+  __shared__ uint32_t s_grab;
+  if (threadIdx.x == 0) s_grab = 0;
   copy_lds_image<kLdsBytesV2>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
   __syncthreads();
   const uint8_t *lds = reinterpret_cast<const uint8_t *>(s_lds);
@@ -121,16 +128,20 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   const bool wlane = hi == 0u && lo >= 8u; // looks up the carried W
   const uint32_t hi8 = 8u * hi;
 
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * 16u;
   const uint32_t nblk = gridDim.x;
   // XCD-aware wave numbering (see crc32_rows_kernel): neighbouring slices, and
   // so neighbouring outputs, live on one XCD.
   const uint32_t vb = (nblk % 8u == 0u) ? (blockIdx.x % 8u) * (nblk / 8u) + blockIdx.x / 8u : blockIdx.x;
-  const uint64_t gw = (uint64_t)vb * 16u + wave;
   const uint64_t nslices = ld_const(a.plan, 0);
-  if (gw >= nslices) return;
   const uint32_t mode = a.mode;
+  auto grab = [&]() -> uint32_t { // lane 0 holds the grabbed k; read a step later
+    uint32_t k = 0;
+    if (lane == 0) k = __hip_atomic_fetch_add(&s_grab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return k;
+  };
+  const uint64_t s0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)grab()) * nblk + vb;
+  if (s0 >= nslices) return;
+  uint32_t pend = grab();
 
   Cursor cur;
   const uint64_t last_body = a.n_items - 1;
@@ -147,9 +158,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
     cur.nb_off = ld_const(a.offsets, nb);
     cur.nb_len = ld_const(a.lengths, nb);
   };
-  auto prefetch_slice = [&]() { // record of slice s + nwaves (clamped in range)
-    uint64_t sl = cur.s + nwaves;
-    if (sl >= nslices) sl = nslices - 1;
+  auto prefetch_slice = [&]() { // the wave's next slice (grabbed a step ago) and its record
+    cur.ns_s = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)pend) * nblk + vb;
+    if (cur.ns_s < nslices) pend = grab();
+    const uint64_t sl = cur.ns_s < nslices ? cur.ns_s : nslices - 1;
     cur.ns = rec(sl);
     cur.ns_end = ld_const(recw, 4 * (sl + 1));
   };
@@ -170,7 +182,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
         enter(cur.nb_off, cur.nb_len);
         prefetch_body();
       } else { // next slice of this wave
-        cur.s += nwaves;
+        cur.s = cur.ns_s;
         if (cur.s >= nslices) {
           cur.done = true;
           return false;
@@ -187,10 +199,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   };
 
   {
-    const SliceRec r0 = rec(gw);
-    cur.s = gw;
+    const SliceRec r0 = rec(s0);
+    cur.s = s0;
     cur.b = r0.b;
-    cur.bend = ld_const(recw, 4 * (gw + 1));
+    cur.bend = ld_const(recw, 4 * (s0 + 1));
     cur.done = false;
     if (cur.b < cur.bend) enter(r0.off, r0.len);
     else cur.nch = cur.k = 0;
@@ -226,7 +238,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   auto issue = [&](Quarter (&q)[4], u32x4 (&buf)[4]) {
     uint64_t p[4];
     bool full;
-    if (!cur.done && cur.k + 4u <= cur.nch) {
+    if (settle() && cur.k + 4u <= cur.nch) {
       // Common case: the next four chunks all belong to the current body.
       // Only quarter 0 can be its first chunk and only quarter 3 its last.
       const uint64_t wend0 = cur.p0 + (uint64_t)cur.len + cur.z - (uint64_t)(cur.nch - 1u - cur.k) * kChunk;
