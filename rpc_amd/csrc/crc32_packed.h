@@ -107,8 +107,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   using namespace packed;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
   // Workgroup-dynamic slice dealing (as the rows kernel's DYN): workgroup vb
-  // owns slices k * blocks + vb, k = 0, 1, ..., and its waves take the next k
-  // from this LDS counter, so they finish together.
+  // owns rounds of 16 consecutive slices, round r = slices (r * blocks + vb) * 16
+  // + [0, 16), and its waves take the next slice from this LDS counter, so they
+  // finish together and neighbouring bodies (and their metadata cache lines)
+  // are walked by one CU at about the same time.
   __shared__ uint32_t s_grab;
   if (threadIdx.x == 0) s_grab = 0;
   copy_lds_image<kLdsBytesV2>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
@@ -139,7 +141,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
     if (lane == 0) k = __hip_atomic_fetch_add(&s_grab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return k;
   };
-  const uint64_t s0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)grab()) * nblk + vb;
+  auto slice_of = [&](uint32_t k) -> uint64_t { return ((uint64_t)(k >> 4) * nblk + vb) * 16u + (k & 15u); };
+  const uint64_t s0 = slice_of((uint32_t)__builtin_amdgcn_readfirstlane((int)grab()));
   if (s0 >= nslices) return;
   uint32_t pend = grab();
 
@@ -159,7 +162,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
     cur.nb_len = ld_const(a.lengths, nb);
   };
   auto prefetch_slice = [&]() { // the wave's next slice (grabbed a step ago) and its record
-    cur.ns_s = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)pend) * nblk + vb;
+    cur.ns_s = slice_of((uint32_t)__builtin_amdgcn_readfirstlane((int)pend));
     if (cur.ns_s < nslices) pend = grab();
     const uint64_t sl = cur.ns_s < nslices ? cur.ns_s : nslices - 1;
     cur.ns = rec(sl);
