@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     p.add_argument("--nontemporal", type=int, default=-1, help="-1 = library default")
     p.add_argument("--ragged-path", default="auto", choices=["auto", "rows", "packed"],
-                   help="ragged-batch kernel (C2): packed = 1 KiB chunks four per row (default for n >= 64)")
+                   help="ragged-batch kernel (C2): auto = rows for device batches; packed = 1 KiB chunks four per row")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
@@ -341,7 +341,7 @@ def main():
                 "frac": round(achieved / (HBM_PEAK_BPS / 1e9), 4),
                 "traffic": traffic,
                 "kernel": {"uniform": "crc32_rows_kernel",
-                           "ragged": "crc32_packed_kernel (+count/scan/plan)" if args.ragged_path != "rows"
+                           "ragged": "crc32_packed_kernel (+count/scan/plan)" if args.ragged_path == "packed"
                            else "crc32_rows_kernel",
                            "large": "crc32_rows_kernel (+chunk combine)"}[w.kind],
                 "avg_launch_us": round(kernel_s * 1e6, 2),

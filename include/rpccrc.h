@@ -169,7 +169,8 @@ RPCCRC_API int rpc_crc32_set_options(int nontemporal, int max_blocks);
 
 /* Kernel for ragged device batches (process-wide; used by rpc_crc32_device_batch,
  * rpc_crc32_batch and the frames calls).  Results are identical either way.
- *   RPCCRC_RAGGED_AUTO   packed for n >= 64 bodies, rows below (default)
+ *   RPCCRC_RAGGED_AUTO   frames calls (bodies <= MAX_BODY_LEN): packed for
+ *                        n >= 64; other batches: rows (default)
  *   RPCCRC_RAGGED_ROWS   one wavefront per body, 4 KiB rows
  *   RPCCRC_RAGGED_PACKED 1 KiB chunks of consecutive bodies packed four per
  *                        row, balanced by chunk count

@@ -225,8 +225,9 @@ RAGGED_PATHS = {"auto": 0, "rows": 1, "packed": 2}
 
 
 def set_ragged_path(path="auto"):
-    """Kernel for ragged device batches: "auto", "rows" (one wavefront per body)
-    or "packed" (1 KiB chunks of consecutive bodies, four per row)."""
+    """Kernel for ragged device batches: "auto" (frames: packed, other batches: rows),
+    "rows" (one wavefront per body) or "packed" (1 KiB chunks of consecutive
+    bodies, four per row)."""
     code = RAGGED_PATHS[path] if isinstance(path, str) else int(path)
     check(_lib.rpc_crc32_set_ragged_path(code), "rpc_crc32_set_ragged_path")
 

@@ -139,13 +139,15 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   return map_hip(launch_rows(a, QB, g_nontemporal != 0, max_blocks_for(c), s));
 }
 
-// A ragged batch on the device: the packed kernel (crc32_packed.h) for many
-// bodies, the rows kernel (one wave per body) for a few.
+// A ragged batch on the device.  AUTO: frames (bodies capped at MAX_BODY_LEN =
+// 1 KiB, rpc.h:17) take the packed kernel (crc32_packed.h: four bodies per
+// row; 1.6x the rows kernel on 1M x 1 KiB), other batches the
+// rows kernel (one wave per body; ahead on C2's 64 B - 64 KiB mix).
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-           uint32_t mode, uint32_t *out, hipStream_t s) {
+           uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies = false) {
   const bool fits = n < 0xFFFFFFFFull;
   const bool packed = fits && (g_ragged_path == RPCCRC_RAGGED_PACKED ||
-                               (g_ragged_path == RPCCRC_RAGGED_AUTO && n >= kPackedMinBodies));
+                               (g_ragged_path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies));
   if (!packed) return items(c, base, offsets, lengths, n, 0, 0, mode, out, 1, s);
   const uint64_t ms = std::min<uint64_t>(kPackedMaxSlices, std::max<uint64_t>(8192, 4 * n));
   size_t bytes = 0;
@@ -565,7 +567,7 @@ int rpc_frames_verify_device(const uint8_t *d_stream, const uint64_t *d_frame_of
   uint32_t *bexp = blen + n;
   uint32_t *bcrc = d_crc ? d_crc : bexp + n;
   rc = map_hip(launch_frames_parse(d_stream, d_frame_offsets, n, boff, blen, bexp, s));
-  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s);
+  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true);
   if (rc == RPCCRC_OK) rc = map_hip(launch_frames_compare(bcrc, bexp, n, d_ok, s));
   (void)hipFreeAsync(ws, s);
   return rc;
@@ -584,7 +586,7 @@ int rpc_frames_stamp_device(uint8_t *d_stream, const uint64_t *d_frame_offsets, 
   uint64_t *boff = reinterpret_cast<uint64_t *>(ws);
   uint32_t *bcrc = reinterpret_cast<uint32_t *>(boff + n);
   rc = map_hip(launch_frames_body_offsets(d_frame_offsets, n, boff, s));
-  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, d_body_lens, n, kModeFinal, bcrc, s);
+  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, d_body_lens, n, kModeFinal, bcrc, s, true);
   if (rc == RPCCRC_OK)
     rc = map_hip(launch_frames_stamp(d_stream, d_frame_offsets, d_body_lens, bcrc, n, version, type, s));
   (void)hipFreeAsync(ws, s);

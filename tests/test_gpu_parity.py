@@ -411,18 +411,18 @@ def test_c2_ragged_loguniform_sample():
     base = torch.empty(total + 8, dtype=torch.uint8, device=DEV)
     rpc_amd.fill_random(base, 0x5EED0004)
     doffs, dlens = to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))
-    got = u32(rpc_amd.device_batch(base, doffs, dlens))  # auto: the packed kernel
+    got = u32(rpc_amd.device_batch(base, doffs, dlens))  # auto: the rows kernel
     rng = np.random.default_rng(4)
     for i in rng.choice(n, 1500, replace=False):
         body = base[int(offs[i]):int(offs[i]) + int(lens[i])].cpu().numpy()
         assert got[i] == oracle.crc32(body), int(i)
     # every body: the two ragged kernels agree
-    rpc_amd.set_ragged_path("rows")
+    rpc_amd.set_ragged_path("packed")
     try:
-        rows = u32(rpc_amd.device_batch(base, doffs, dlens))
+        packed = u32(rpc_amd.device_batch(base, doffs, dlens))
     finally:
         rpc_amd.set_ragged_path("auto")
-    assert np.array_equal(got, rows)
+    assert np.array_equal(got, packed)
 
 
 def test_c4_large_bodies():
