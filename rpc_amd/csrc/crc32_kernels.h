@@ -56,6 +56,7 @@ struct PackedBatch {
   void *ws;
   size_t ws_bytes;
   uint64_t max_slices; // slice-table capacity (balance granularity)
+  uint64_t min_slice;  // chunks per slice, at least
 };
 hipError_t packed_workspace_bytes(uint64_t n, uint64_t max_slices, size_t *bytes);
 hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hipStream_t stream);

@@ -167,7 +167,6 @@ hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream) {
 // are stream-ordered; nothing here waits on the device.
 // ---------------------------------------------------------------------------
 namespace {
-constexpr uint64_t kPackedMinSlice = 8; // chunks per slice, at least
 
 __global__ void __launch_bounds__(256) packed_count_kernel(const uint8_t *base, const uint64_t *offsets,
                                                            const uint32_t *lengths, uint64_t n, uint32_t *cnt,
@@ -184,12 +183,13 @@ __global__ void __launch_bounds__(256) packed_count_kernel(const uint8_t *base, 
 // sentinel {n, 0, 0}, up to nslices).
 __global__ void __launch_bounds__(256) packed_plan_kernel(const uint64_t *cfirst, const uint32_t *cnt,
                                                           const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-                                                          uint64_t max_slices, uint4 *slice_rec, uint64_t *plan) {
+                                                          uint64_t max_slices, uint64_t min_slice, uint4 *slice_rec,
+                                                          uint64_t *plan) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i > n) return;
   const uint64_t total = cfirst[n - 1] + cnt[n - 1];
   uint64_t S = (total + max_slices - 1) / max_slices;
-  if (S < kPackedMinSlice) S = kPackedMinSlice;
+  if (S < min_slice) S = min_slice;
   const uint64_t nslices = (total + S - 1) / S;
   if (i == 0) {
     plan[0] = nslices;
@@ -221,7 +221,7 @@ hipError_t packed_workspace_bytes(uint64_t n, uint64_t max_slices, size_t *bytes
 
 hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hipStream_t s) {
   if (p.n == 0) return hipSuccess;
-  if (p.n >= 0xFFFFFFFFull || p.max_slices == 0) return hipErrorInvalidValue;
+  if (p.n >= 0xFFFFFFFFull || p.max_slices == 0 || p.min_slice == 0) return hipErrorInvalidValue;
   uint8_t *w = static_cast<uint8_t *>(p.ws);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(w);
   w += align256(p.n * 4);
@@ -241,7 +241,7 @@ hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hi
   e = packed_scan(w, scan, cnt, cfirst, p.n, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(packed_plan_kernel, dim3((unsigned)((p.n + 1 + 255) / 256)), dim3(256), 0, s, cfirst, cnt,
-                     p.offsets, p.lengths, p.n, p.max_slices, slices, plan);
+                     p.offsets, p.lengths, p.n, p.max_slices, p.min_slice, slices, plan);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   PackedArgs a;

@@ -13,9 +13,11 @@
 // SLICES of S chunks; a body belongs to the slice its first chunk lies in and
 // slice_rec[s] holds the first body of slice s.  Slices are dealt round-robin
 // over the workgroups (a moving window over HBM, like the rows kernel), the
-// waves of a workgroup take its slices from an LDS counter, and a wave
-// walks the bodies of its slices with a scalar cursor, packing chunks across
-// body and slice boundaries.  A body is always processed start to end by ONE
+// waves of a workgroup take its slices from an LDS counter, and a wave walks
+// the bodies of its slices through a 64-body metadata WINDOW (one body per
+// lane, loaded a row ahead with vector loads; a prefix scan of the chunk
+// counts and one ballot per quarter find the body of each chunk), packing
+// chunks across body and slice boundaries.  A body is always processed start to end by ONE
 // wave (past its slice's end if need be), so the Horner chain across rows stays
 // inside the wave: no cross-wave combine and no buffer sized by the chunk count.
 //
@@ -52,9 +54,9 @@ namespace packed {
 
 constexpr uint32_t kChunk = 1024;
 
-// Plan record of slice s: its first body and that body's offset / length, so a
-// wave enters a slice with one scalar load (prefetched a slice ahead) instead
-// of a chain slice table -> body table.  Record nslices is the sentinel {n}.
+// Plan record of slice s: its first body (the kernel reads only .b; the
+// body's offset / length ride along for tools).  Record nslices is the
+// sentinel {n}.
 struct SliceRec {
   uint32_t b;
   uint32_t len;
@@ -71,33 +73,29 @@ __host__ __device__ __forceinline__ uint32_t body_chunks(uint64_t end, uint32_t 
 
 // Quarter descriptor, carried from issue to compute (wave-uniform).
 constexpr uint32_t kQFirst = 1u << 15, kQLast = 1u << 16, kQValid = 1u << 17;
+constexpr uint32_t kQLive = 1u << 18; // quarter 0 only: the wave's stream was not finished at issue
 struct Quarter {
   uint32_t info; // clen (bits 0-10) | z << 11 | first << 15 | last << 16 | valid << 17
   uint32_t body;
-  uint32_t seed; // A_{clen+z}(0xFFFFFFFF) on a body's first chunk (kModeFinal), else 0
+  uint32_t lane; // window lane of the body (its seed is read from that lane)
 };
 __device__ __forceinline__ uint32_t q_clen(uint32_t i) { return i & 0x7FFu; }
 __device__ __forceinline__ uint32_t q_z(uint32_t i) { return (i >> 11) & 15u; }
 
-// The wave's scalar cursor.  Body b+1's metadata and the next slice's record
-// are loaded one step ahead, so moving to a new body or slice issues loads but
-// never waits on one in the issue path.
-struct Cursor {
-  uint64_t s;      // current slice
-  uint64_t p0;     // start address of body b
-  uint32_t b;      // current body
-  uint32_t bend;   // first body of the next slice (bodies [., bend) are ours)
-  uint32_t k;      // next chunk of body b
-  uint32_t nch;    // chunks of body b
-  uint32_t len;
-  uint32_t z;
-  uint64_t nb_off; // body b+1 (prefetched)
-  uint32_t nb_len;
-  uint64_t ns_s;   // the wave's next slice,
-  SliceRec ns;     // its record (prefetched) and its end body
-  uint32_t ns_end;
-  bool done;
-};
+// Exclusive prefix sum over the 64 lanes: row_shr 1/2/4/8 inside each 16-lane
+// row (bound_ctrl: lanes shifted in read 0), then the row totals by readlane.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane) {
+  uint32_t v = x;
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x118, 0xF, 0xF, true);
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+  const uint32_t r1 = r0 + (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+  const uint32_t r2 = r1 + (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+  const uint32_t add = lane >= 48u ? r2 : lane >= 32u ? r1 : lane >= 16u ? r0 : 0u;
+  return v + add - x;
+}
 
 } // namespace packed
 
@@ -136,152 +134,185 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   const uint32_t vb = (nblk % 8u == 0u) ? (blockIdx.x % 8u) * (nblk / 8u) + blockIdx.x / 8u : blockIdx.x;
   const uint64_t nslices = ld_const(a.plan, 0);
   const uint32_t mode = a.mode;
+  const uint64_t base = (uint64_t)(uintptr_t)a.base;
   auto grab = [&]() -> uint32_t { // lane 0 holds the grabbed k; read a step later
     uint32_t k = 0;
     if (lane == 0) k = __hip_atomic_fetch_add(&s_grab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return k;
   };
   auto slice_of = [&](uint32_t k) -> uint64_t { return ((uint64_t)(k >> 4) * nblk + vb) * 16u + (k & 15u); };
-  const uint64_t s0 = slice_of((uint32_t)__builtin_amdgcn_readfirstlane((int)grab()));
-  if (s0 >= nslices) return;
-  uint32_t pend = grab();
-
-  Cursor cur;
-  const uint64_t last_body = a.n_items - 1;
   const uint32_t *recw = reinterpret_cast<const uint32_t *>(a.slice_rec);
-  auto rec = [&](uint64_t sl) -> SliceRec { // one s_load_dwordx4
-    SliceRec x;
-    x.b = ld_const(recw, 4 * sl);
-    x.len = ld_const(recw, 4 * sl + 1);
-    x.off = (uint64_t)ld_const(recw, 4 * sl + 2) | ((uint64_t)ld_const(recw, 4 * sl + 3) << 32);
-    return x;
-  };
-  auto prefetch_body = [&]() { // body b+1 (an in-range index either way)
-    const uint64_t nb = (uint64_t)cur.b + 1 <= last_body ? (uint64_t)cur.b + 1 : last_body;
-    cur.nb_off = ld_const(a.offsets, nb);
-    cur.nb_len = ld_const(a.lengths, nb);
-  };
-  auto prefetch_slice = [&]() { // the wave's next slice (grabbed a step ago) and its record
-    cur.ns_s = slice_of((uint32_t)__builtin_amdgcn_readfirstlane((int)pend));
-    if (cur.ns_s < nslices) pend = grab();
-    const uint64_t sl = cur.ns_s < nslices ? cur.ns_s : nslices - 1;
-    cur.ns = rec(sl);
-    cur.ns_end = ld_const(recw, 4 * (sl + 1));
-  };
-  auto enter = [&](uint64_t off, uint32_t len) { // body b with this metadata becomes current
-    cur.len = len;
-    cur.p0 = (uint64_t)(uintptr_t)a.base + off;
-    cur.z = (uint32_t)(0u - (uint32_t)(cur.p0 + len)) & 15u;
-    cur.nch = body_chunks(cur.p0 + len, len);
-    cur.k = 0;
-  };
-  // Move the cursor onto its next chunk (next body, next slice of this wave);
-  // false once the wave's slices are exhausted.
-  auto settle = [&]() -> bool {
-    if (cur.done) return false;
-    while (cur.k >= cur.nch) {
-      if (cur.b + 1u < cur.bend) { // next body of this slice
-        ++cur.b;
-        enter(cur.nb_off, cur.nb_len);
-        prefetch_body();
-      } else { // next slice of this wave
-        cur.s = cur.ns_s;
-        if (cur.s >= nslices) {
-          cur.done = true;
-          return false;
-        }
-        cur.b = cur.ns.b;
-        cur.bend = cur.ns_end;
-        if (cur.b < cur.bend) enter(cur.ns.off, cur.ns.len);
-        else cur.nch = cur.k = 0; // empty slice (inside a long body of an earlier one)
-        prefetch_body();
-        prefetch_slice();
+
+  // The wave's stream is the concatenation of the bodies of its slices.  It
+  // keeps two slices: the current one, bodies [wb0, cb1) still to walk, and the
+  // next one, [nb0, nb1) (empty once the wave's slices are exhausted).
+  uint32_t pend = grab();
+  uint32_t wb0 = 0, cb1 = 0, nb0 = 0, nb1 = 0;
+  bool more_slices = true;
+  auto fetch_next = [&]() { // next non-empty slice of this wave into [nb0, nb1)
+    nb0 = nb1 = 0;
+    while (more_slices) {
+      const uint64_t sl = slice_of((uint32_t)__builtin_amdgcn_readfirstlane((int)pend));
+      if (sl >= nslices) {
+        more_slices = false;
+        break;
       }
+      pend = grab();
+      nb0 = ld_const(recw, 4 * sl);
+      nb1 = ld_const(recw, 4 * (sl + 1));
+      if (nb0 < nb1) break;
     }
-    return true;
   };
-
-  {
-    const SliceRec r0 = rec(s0);
-    cur.s = s0;
-    cur.b = r0.b;
-    cur.bend = ld_const(recw, 4 * (s0 + 1));
-    cur.done = false;
-    if (cur.b < cur.bend) enter(r0.off, r0.len);
-    else cur.nch = cur.k = 0;
-    prefetch_body();
-    prefetch_slice();
-  }
-  if (!settle()) return;
-  const uint64_t safe = cur.p0 & ~(uint64_t)15; // 16-B block of a byte this wave reads
-
-  // The next chunk of the wave's stream as one quarter of the row being issued.
-  auto take = [&](Quarter &q, uint64_t &qp0) {
-    if (!settle()) {
-      q.info = 0;
-      q.body = 0;
-      q.seed = 0;
-      qp0 = safe;
-      return;
-    }
-    const uint64_t v = (uint64_t)cur.len + cur.z;
-    const uint64_t wend = cur.p0 + v - (uint64_t)(cur.nch - 1u - cur.k) * kChunk; // 16-B aligned
-    const bool first = cur.k == 0, last = cur.k + 1u == cur.nch;
-    const uint64_t rs = first ? cur.p0 : wend - kChunk; // real bytes [rs, re)
-    const uint64_t re = last ? cur.p0 + cur.len : wend;
-    const uint32_t clen = (uint32_t)(re - rs);
-    const uint32_t z = last ? cur.z : 0u;
-    q.info = clen | (z << 11) | (first ? kQFirst : 0u) | (last ? kQLast : 0u) | kQValid;
-    q.body = cur.b;
-    q.seed = (first && mode != kModeRaw) ? ld_const(a.tq, clen + z) : 0u;
-    qp0 = rs;
-    ++cur.k;
+  auto advance = [&]() { // the next slice becomes current
+    wb0 = nb0;
+    cb1 = nb1;
+    fetch_next();
   };
+  fetch_next();
+  advance();
+  if (wb0 >= cb1) return; // no slice for this wave
+  uint32_t wk0 = 0;       // chunk of body wb0 where the next row starts
 
-  auto issue = [&](Quarter (&q)[4], u32x4 (&buf)[4]) {
+  // WINDOW: the next 64 bodies of the stream, one per lane (lane l < kw: body
+  // wb0 + l of the current slice; lane l >= kw: body nb0 + l - kw of the next
+  // one), loaded a row ahead with two vector loads and decoded with ballots
+  // and readlanes -- no scalar body walk.  Lanes past the stream read zeros.
+  const auto off_rsrc = row_rsrc((uint64_t)(uintptr_t)a.offsets);
+  const auto len_rsrc = row_rsrc((uint64_t)(uintptr_t)a.lengths);
+  const auto tq_rsrc = row_rsrc((uint64_t)(uintptr_t)a.tq);
+  uint32_t w_kw = 0, w_b0 = 0, w_n0 = 0, w_n1 = 0; // the window's layout, fixed when it was loaded
+  uint32_t w_offlo = 0, w_offhi = 0, w_len = 0;
+  auto load_window = [&]() {
+    w_kw = (cb1 - wb0) < 64u ? cb1 - wb0 : 64u;
+    w_b0 = wb0;
+    w_n0 = nb0;
+    w_n1 = nb1;
+    const uint32_t idx = lane < w_kw ? w_b0 + lane : w_n0 + (lane - w_kw);
+    const bool ok = lane < w_kw || idx < w_n1;
+    const auto o = __builtin_amdgcn_raw_buffer_load_b64(off_rsrc, ok ? (int)(idx * 8u) : (int)kOobOffset, 0, 0);
+    w_offlo = o[0];
+    w_offhi = o[1];
+    w_len = __builtin_amdgcn_raw_buffer_load_b32(len_rsrc, ok ? (int)(idx * 4u) : (int)kOobOffset, 0, 0);
+  };
+  load_window();
+
+  auto issue = [&](Quarter (&q)[4], u32x4 (&buf)[4], uint32_t &seedv) {
+    // Decode the window: pads, chunk counts and each body's first chunk in
+    // window chunk coordinates (body wb0's chunk 0 = position 0).
+    const uint32_t endlo = (uint32_t)base + w_offlo + w_len;
+    const uint32_t zl = (0u - endlo) & 15u;
+    const uint32_t vl = w_len + zl;
+    const uint32_t nchl = w_len ? (vl + kChunk - 1u) >> 10 : 0u;
+    const uint32_t cst = wave_excl_scan(nchl, lane);
+    const bool has = nchl != 0u;
+    // zlib seed of the body's first chunk, A_{first window fill}(0xFFFFFFFF)
+    seedv = __builtin_amdgcn_raw_buffer_load_b32(tq_rsrc, has ? (int)((vl - ((nchl - 1u) << 10)) * 4u) : (int)kOobOffset,
+                                                 0, 0);
+    uint32_t nvalid = 4u;
     uint64_t p[4];
-    bool full;
-    if (settle() && cur.k + 4u <= cur.nch) {
-      // Common case: the next four chunks all belong to the current body.
-      // Only quarter 0 can be its first chunk and only quarter 3 its last.
-      const uint64_t wend0 = cur.p0 + (uint64_t)cur.len + cur.z - (uint64_t)(cur.nch - 1u - cur.k) * kChunk;
-      const bool first = cur.k == 0, last = cur.k + 4u == cur.nch;
-      const uint32_t c0 = first ? (uint32_t)(wend0 - cur.p0) : kChunk;
-      const uint32_t c3 = last ? kChunk - cur.z : kChunk;
-      const uint32_t z3 = last ? cur.z : 0u;
-      q[0].info = c0 | (first ? kQFirst : 0u) | kQValid;
-      q[0].seed = (first && mode != kModeRaw) ? ld_const(a.tq, c0) : 0u;
+    auto locate = [&](uint32_t pos, uint32_t &m, uint32_t &c, uint32_t &nc) -> bool { // body lane holding pos
+      const uint64_t m64 = __builtin_amdgcn_ballot_w64(has && cst <= pos);
+      m = m64 ? 63u - (uint32_t)__builtin_clzll(m64) : 0u;
+      c = (uint32_t)__builtin_amdgcn_readlane((int)cst, m);
+      nc = (uint32_t)__builtin_amdgcn_readlane((int)nchl, m);
+      return m64 != 0u && pos - c < nc;
+    };
+    auto body_p0 = [&](uint32_t m, uint32_t &len, uint32_t &z) -> uint64_t {
+      len = (uint32_t)__builtin_amdgcn_readlane((int)w_len, m);
+      const uint64_t p0 = base + ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w_offhi, m) << 32 |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)w_offlo, m));
+      z = (uint32_t)(0u - (uint32_t)(p0 + len)) & 15u;
+      return p0;
+    };
+    uint32_t m0, c0, nc0;
+    const bool v0 = locate(wk0, m0, c0, nc0);
+    const uint32_t body0 = m0 < w_kw ? w_b0 + m0 : w_n0 + (m0 - w_kw);
+    bool known = false; // the next row starts inside body m0
+    if (v0 && wk0 - c0 + 4u <= nc0) {
+      // Common case: the four chunks all belong to one body.  Only quarter 0
+      // can be its first chunk and only quarter 3 its last.
+      uint32_t len, z;
+      const uint64_t p0 = body_p0(m0, len, z);
+      const uint32_t j = wk0 - c0;
+      const uint64_t wend0 = p0 + len + z - (uint64_t)(nc0 - 1u - j) * kChunk; // end of chunk j's window
+      const bool first = j == 0u, last = j + 4u == nc0;
+      q[0].info = (first ? (uint32_t)(wend0 - p0) : kChunk) | (first ? kQFirst : 0u) | kQValid;
       q[1].info = kChunk | kQValid;
-      q[1].seed = 0;
       q[2].info = kChunk | kQValid;
-      q[2].seed = 0;
-      q[3].info = c3 | (z3 << 11) | (last ? kQLast : 0u) | kQValid;
-      q[3].seed = 0;
+      q[3].info = (last ? kChunk - z : kChunk) | ((last ? z : 0u) << 11) | (last ? kQLast : 0u) | kQValid;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) q[b].body = cur.b;
-      p[0] = first ? cur.p0 : wend0 - kChunk;
+      for (int b = 0; b < 4; ++b) {
+        q[b].body = body0;
+        q[b].lane = m0;
+      }
+      p[0] = first ? p0 : wend0 - kChunk;
       p[1] = wend0;
       p[2] = wend0 + kChunk;
       p[3] = wend0 + 2 * kChunk;
-      cur.k += 4u;
-      full = !first && !last;
+      known = !last;
     } else {
-      // Body or slice boundary inside the row: one chunk at a time (one copy
-      // of the cursor code; the quarter index only selects registers).
-      full = true;
-#pragma nounroll
+      // Body boundaries inside the row (or the end of the stream).
+#pragma unroll
       for (int b = 0; b < 4; ++b) {
-        Quarter t;
-        uint64_t tp;
-        take(t, tp);
-        full = full && q_clen(t.info) == kChunk;
-        if (b == 0) { q[0] = t; p[0] = tp; }
-        else if (b == 1) { q[1] = t; p[1] = tp; }
-        else if (b == 2) { q[2] = t; p[2] = tp; }
-        else { q[3] = t; p[3] = tp; }
+        const uint32_t pos = wk0 + (uint32_t)b;
+        uint32_t m = m0, c = c0, nc = nc0;
+        bool valid = v0;
+        if (b > 0) valid = nvalid == 4u && locate(pos, m, c, nc);
+        if (!valid) {
+          if (nvalid == 4u) nvalid = (uint32_t)b;
+          q[b].info = 0;
+          q[b].body = 0;
+          q[b].lane = 0;
+          p[b] = base;
+          continue;
+        }
+        uint32_t len, z;
+        const uint64_t p0 = body_p0(m, len, z);
+        const uint32_t j = pos - c;
+        const uint64_t wend = p0 + len + z - (uint64_t)(nc - 1u - j) * kChunk; // 16-B aligned
+        const bool first = j == 0u, last = j + 1u == nc;
+        const uint64_t rs = first ? p0 : wend - kChunk; // real bytes [rs, re)
+        const uint64_t re = last ? p0 + len : wend;
+        q[b].info = (uint32_t)(re - rs) | ((last ? z : 0u) << 11) | (first ? kQFirst : 0u) | (last ? kQLast : 0u) | kQValid;
+        q[b].body = m < w_kw ? w_b0 + m : w_n0 + (m - w_kw);
+        q[b].lane = m;
+        p[b] = rs;
       }
     }
-    (void)full;
+    if (wb0 < cb1 || nb0 < nb1) q[0].info |= kQLive;
+
+    // Where the next row starts: the body holding position wk0 + nvalid, or
+    // (window exhausted: every lane's chunks taken) the body after the window.
+    {
+      const uint32_t pos = wk0 + nvalid;
+      uint32_t skip; // bodies of the stream before the next row's body
+      uint32_t m = m0, c = c0, nc;
+      if (known || locate(pos, m, c, nc)) {
+        skip = m;
+        wk0 = pos - c;
+      } else {
+        skip = 64u;
+        wk0 = 0;
+      }
+      if (skip < cb1 - wb0) {
+        wb0 += skip;
+      } else {
+        // the current slice is used up; rest bodies into the next
+        uint32_t rest = skip - (cb1 - wb0);
+        advance();
+        while (wb0 < cb1 && rest >= cb1 - wb0) { // the window ran past the next slice too
+          rest = 0;
+          advance();
+        }
+        wb0 += rest;
+      }
+      if (wb0 >= cb1) { // stream finished: later windows are empty
+        wb0 = cb1 = 0;
+        nb0 = nb1 = 0;
+      }
+    }
+    load_window(); // for the next row
+
     // One load path for every row (a separate path for whole rows made the
     // compiler's vmcnt accounting wait for the row just issued): the window of
     // quarter b starts d bytes from the 16-B block holding the chunk's first
@@ -289,9 +320,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const uint32_t clen = q_clen(q[b].info);
-      const uint64_t base = clen ? (p[b] & ~(uint64_t)15) : safe;
       const int32_t d = clen ? (int32_t)(clen + q_z(q[b].info)) - (int32_t)kChunk + (int32_t)(p[b] & 15) : INT32_MIN / 2;
-      buf[b] = ldb16_or_zero<NT>(row_rsrc(base), d + (int32_t)pofs);
+      buf[b] = ldb16_or_zero<NT>(row_rsrc(p[b] & ~(uint64_t)15), d + (int32_t)pofs);
     }
   };
 
@@ -310,14 +340,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
     ocount = 0;
   };
 
-  auto compute = [&](const Quarter (&q)[4], u32x4 (&buf)[4]) {
+  auto compute = [&](const Quarter (&q)[4], u32x4 (&buf)[4], uint32_t seedv) {
     uint32_t sl = 0;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const uint32_t clen = q_clen(q[b].info), z = q_z(q[b].info);
       const int32_t vstart = (int32_t)(clen + z) - (int32_t)kChunk;
       if (vstart < 0 || z != 0u) buf[b] = mask_piece32(buf[b], vstart + (int32_t)pofs, (int32_t)clen);
-      sl = (hi == (uint32_t)b) ? q[b].seed : sl;
+      const bool seeded = (q[b].info & kQFirst) != 0u && mode != kModeRaw;
+      const uint32_t seed = seeded ? (uint32_t)__builtin_amdgcn_readlane((int)seedv, q[b].lane) : 0u;
+      sl = (hi == (uint32_t)b) ? seed : sl;
     }
     const uint32_t v = quarter_crcs(buf) ^ sl; // row hi: q_hi (^ seed on a first chunk)
 
@@ -400,16 +432,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
 
   // One row of loads in flight ahead of the row being computed; one exit at
   // the bottom (see crc32_rows_kernel).  Rows past the wave's stream are
-  // all-invalid: safe loads, no run finishes.
+  // all-invalid: out-of-range loads, no run finishes.
   Quarter qa[4], qb[4];
   u32x4 bufA[4], bufB[4];
-  issue(qa, bufA);
+  uint32_t seedA, seedB;
+  issue(qa, bufA, seedA);
   do {
-    issue(qb, bufB);
-    compute(qa, bufA);
-    issue(qa, bufA);
-    compute(qb, bufB);
-  } while ((qa[0].info & kQValid) != 0u);
+    issue(qb, bufB, seedB);
+    compute(qa, bufA, seedA);
+    issue(qa, bufA, seedA);
+    compute(qb, bufB, seedB);
+  } while ((qa[0].info & kQLive) != 0u);
   flush();
 }
 

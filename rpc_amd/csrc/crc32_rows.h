@@ -125,6 +125,8 @@ __device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
 constexpr uint32_t kRsrcRange = 0x40000000u;
 constexpr uint32_t kOobOffset = 0x7FFFFFF0u;
 static_assert(kOobOffset >= kRsrcRange, "the out-of-range offset must fail the range check");
+// Flags 0x00020000: DATA_FORMAT 32 (a descriptor with format 0, "invalid",
+// reads zeros).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(uint64_t base) {
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)kRsrcRange, 0x00020000);
 }

@@ -48,6 +48,16 @@ int g_ragged_path = RPCCRC_RAGGED_AUTO;
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kPackedMinBodies = 64;         // fewer bodies: one wave per body (rows kernel)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
+// Chunks per packed slice, at least: a slice switch costs the wave two scalar
+// loads it waits on.  Tuning override: RPCCRC_PACKED_MIN_SLICE.
+uint64_t packed_min_slice() {
+  static const uint64_t v = [] {
+    const char *e = getenv("RPCCRC_PACKED_MIN_SLICE");
+    const long long x = e ? atoll(e) : 0;
+    return x > 0 ? (uint64_t)x : (uint64_t)32;
+  }();
+  return v;
+}
 
 int map_hip(hipError_t e) {
   if (e == hipSuccess) return RPCCRC_OK;
@@ -145,7 +155,7 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
 // rows kernel (one wave per body; ahead on C2's 64 B - 64 KiB mix).
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
            uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies = false) {
-  const bool fits = n < 0xFFFFFFFFull;
+  const bool fits = n < (1ull << 27); // the packed kernel's metadata window: 8-B offsets in a 1 GiB buffer range
   const bool packed = fits && (g_ragged_path == RPCCRC_RAGGED_PACKED ||
                                (g_ragged_path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies));
   if (!packed) return items(c, base, offsets, lengths, n, 0, 0, mode, out, 1, s);
@@ -166,6 +176,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   p.ws = ws;
   p.ws_bytes = bytes;
   p.max_slices = ms;
+  p.min_slice = packed_min_slice();
   const int r = map_hip(launch_packed_batch(p, g_nontemporal != 0, max_blocks_for(c), s));
   (void)hipFreeAsync(ws, s);
   return r;

@@ -18,6 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <vector>
 
 using namespace rpccrc;
@@ -245,8 +246,8 @@ static void emu_qb4(const uint8_t *const p0[4], const uint32_t len[4], int nvali
 }
 
 // ---- packed ragged kernel (crc32_packed.h) ------------------------------------
-// The plan (chunk counts, exclusive scan, slice table), every wave's scalar
-// cursor over its slices, rows of four 1 KiB chunks, the distributed run shift
+// The plan (chunk counts, exclusive scan, slice table), every wave's 64-body
+// metadata window over its slices (prefix scan + ballots), rows of four 1 KiB chunks, the distributed run shift
 // (ST2 / RW), the scalar run XOR and the distributed ZI step of finished bodies.
 // Checks that every slice is planned once and every body is written once.
 
@@ -294,40 +295,72 @@ static void emu_packed(const std::vector<const uint8_t *> &ptr, const std::vecto
     if (sb[s] == 0xFFFFFFFFu) { fprintf(stderr, "slice %llu unplanned\n", (unsigned long long)s); exit(5); }
 
   for (uint64_t gw = 0; gw < nwaves && gw < nslices; ++gw) {
-    uint64_t s = gw;
-    uint32_t b = sb[gw] - 1u, bend = sb[gw + 1], k = 0, nch = 0, len = 0, z = 0;
-    const uint8_t *p0 = nullptr;
-    bool done = false;
-    auto settle = [&]() -> bool {
-      if (done) return false;
-      while (k >= nch) {
-        ++b;
-        while (b >= bend) {
-          s += nwaves;
-          if (s >= nslices) {
-            done = true;
-            return false;
-          }
-          b = sb[s];
-          bend = sb[s + 1];
+    // The wave's stream (crc32_packed.h): current slice [wb0, cb1), next
+    // slice [nb0, nb1); slices dealt round-robin here (the kernel deals them
+    // dynamically; any order gives the same CRCs).
+    uint64_t snext = gw;
+    bool more = true;
+    uint32_t wb0 = 0, cb1 = 0, nb0 = 0, nb1 = 0, wk0 = 0;
+    auto fetch_next = [&]() {
+      nb0 = nb1 = 0;
+      while (more) {
+        if (snext >= nslices) {
+          more = false;
+          break;
         }
-        len = lens[b];
-        p0 = ptr[b];
-        z = (uint32_t)(0u - (uint32_t)((uintptr_t)p0 + len)) & 15u;
-        nch = pk_body_chunks((uint64_t)(uintptr_t)p0 + len, len);
-        k = 0;
+        const uint64_t sl = snext;
+        snext += nwaves;
+        nb0 = sb[sl];
+        nb1 = sb[sl + 1];
+        if (nb0 < nb1) break;
       }
-      return true;
     };
-    if (!settle()) continue;
+    auto advance = [&]() {
+      wb0 = nb0;
+      cb1 = nb1;
+      fetch_next();
+    };
+    fetch_next();
+    advance();
+    if (wb0 >= cb1) continue;
     uint32_t W = 0;
     for (;;) {
+      // window: 64 bodies of the stream, one per lane
+      const uint32_t kw = std::min<uint32_t>(64u, cb1 - wb0), wn0 = nb0, wn1 = nb1, w0 = wb0;
+      uint32_t idx[64], wl[64], nchl[64], cst[64];
+      bool has[64];
+      uint32_t run = 0;
+      for (uint32_t l = 0; l < 64; ++l) {
+        idx[l] = l < kw ? w0 + l : wn0 + (l - kw);
+        const bool ok = l < kw || idx[l] < wn1;
+        wl[l] = ok ? lens[idx[l]] : 0u;
+        const uint32_t z = ok ? (uint32_t)(0u - (uint32_t)((uintptr_t)ptr[idx[l]] + wl[l])) & 15u : 0u;
+        nchl[l] = wl[l] ? (wl[l] + z + 1023u) >> 10 : 0u;
+        has[l] = nchl[l] != 0;
+        cst[l] = run;
+        run += nchl[l];
+      }
+      auto find = [&](uint32_t pos, uint32_t &m) -> bool { // last nonempty lane with cst <= pos
+        int mm = -1;
+        for (int l = 0; l < 64; ++l)
+          if (has[l] && cst[l] <= pos) mm = l;
+        m = mm < 0 ? 0u : (uint32_t)mm;
+        return mm >= 0 && pos - cst[m] < nchl[m];
+      };
       PkQuarter q[4];
+      uint32_t nvalid = 4;
       for (int bq = 0; bq < 4; ++bq) {
-        if (!settle()) continue;
-        const uint64_t v = (uint64_t)len + z;
-        const uint8_t *wend = p0 + v - (uint64_t)(nch - 1 - k) * 1024;
-        const bool first = k == 0, last = k + 1 == nch;
+        uint32_t m;
+        const uint32_t pos = wk0 + (uint32_t)bq;
+        if (nvalid != 4 || !find(pos, m)) {
+          if (nvalid == 4) nvalid = (uint32_t)bq;
+          continue;
+        }
+        const uint32_t j = pos - cst[m], nc = nchl[m], len = wl[m];
+        const uint8_t *p0 = ptr[idx[m]];
+        const uint32_t z = (uint32_t)(0u - (uint32_t)((uintptr_t)p0 + len)) & 15u;
+        const uint8_t *wend = p0 + len + z - (uint64_t)(nc - 1 - j) * 1024;
+        const bool first = j == 0, last = j + 1 == nc;
         const uint8_t *rs = first ? p0 : wend - 1024;
         const uint8_t *re = last ? p0 + len : wend;
         q[bq].clen = (uint32_t)(re - rs);
@@ -335,12 +368,36 @@ static void emu_packed(const std::vector<const uint8_t *> &ptr, const std::vecto
         q[bq].first = first;
         q[bq].last = last;
         q[bq].valid = true;
-        q[bq].body = b;
-        q[bq].seed = first ? g_tq[q[bq].clen + q[bq].z] : 0;
+        q[bq].body = idx[m];
+        // seed: the first window fill of lane m's body (kernel: tq gather per lane)
+        q[bq].seed = first ? g_tq[len + z - (nc - 1) * 1024] : 0;
         q[bq].p = rs;
-        ++k;
       }
-      if (!q[0].valid) break;
+      const bool live = wb0 < cb1 || nb0 < nb1;
+      { // next row start
+        uint32_t m, skip;
+        const uint32_t pos = wk0 + nvalid;
+        if (find(pos, m)) {
+          skip = m;
+          wk0 = pos - cst[m];
+        } else {
+          skip = 64;
+          wk0 = 0;
+        }
+        if (skip < cb1 - wb0) {
+          wb0 += skip;
+        } else {
+          uint32_t rest = skip - (cb1 - wb0);
+          advance();
+          while (wb0 < cb1 && rest >= cb1 - wb0) {
+            rest = 0;
+            advance();
+          }
+          wb0 += rest;
+        }
+        if (wb0 >= cb1) wb0 = cb1 = nb0 = nb1 = 0;
+      }
+      if (!live) break;
       static Piece P[4][64];
       for (int bq = 0; bq < 4; ++bq) {
         const int64_t vstart = (int64_t)q[bq].clen + q[bq].z - 1024;

@@ -79,7 +79,8 @@ def test_emulated_packed_kernel_matches_oracle(rows_emu, mis, nwaves, min_slice,
     inside a long body, waves with no work."""
     rng = np.random.default_rng(mis * 131 + nwaves * 7 + min_slice)
     lens = (LENS + [0, 0, 1, 0, 1024, 1023, 1025, 2048, 3072, 4096, 5000] + rng.integers(0, 200, 40).tolist()
-            + rng.integers(0, 9000, 12).tolist() + [0, 70000, 2, 0, 17])
+            + rng.integers(0, 9000, 12).tolist() + [0, 70000, 2, 0, 17]
+            + [0] * 150 + [5] + [0] * 64 + [3000] + [0] * 63 + rng.integers(1, 40, 200).tolist() + [0] * 70)
     inp = f"2 {mis} {len(lens)} {nwaves} {min_slice} {max_slices}\n" + "\n".join(map(str, lens)) + "\n"
     out = subprocess.run([rows_emu], input=inp.encode(), capture_output=True, check=True).stdout.decode().split()
     assert len(out) == len(lens)

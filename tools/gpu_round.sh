@@ -45,6 +45,17 @@ for s in $STEPS; do
     timeline_save) run timeline_save 300 python tools/probe.py --mode timeline --reps 2 --save $OUT/tl_g0 ;;
     ablate_dyn) run ablate_dyn 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl0_d1_g3,qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl1027_d1,qb1_pair1_nt1_abl19_d1,qb1_pair1_nt1_abl1043_d1 ;;
     timeline_dyn) run timeline_dyn 300 python tools/probe.py --mode timeline --reps 2 --dyn --save $OUT/tl_dyn ;;
+    packed_slice)
+           for m in 32 128 512; do
+             RPCCRC_PACKED_MIN_SLICE=$m run packed_s$m 300 python tools/probe.py --mode packed --rounds 3 --reps 5 --shapes 4096x1M,1024x1M,c2 --paths packed || exit 1
+           done ;;
+    packed_slice_small)
+           for m in 8 16; do
+             RPCCRC_PACKED_MIN_SLICE=$m run packed_s$m 300 python tools/probe.py --mode packed --rounds 3 --reps 5 --shapes 4096x1M,1024x1M,c2 --paths rows,packed || exit 1
+           done ;;
+    pmcpacked)
+           run pmcpacked 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
+               -d "$OUT/pmcpacked" -o run --output-format csv -- python3 tools/probe.py --mode packed --rounds 1 --reps 2 --shapes 4096x1M,1024x1M ;;
     packed) run packed 600 python tools/probe.py --mode packed --rounds 3 --reps 5 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;

@@ -173,6 +173,8 @@ def packed_modes(a):
     res = []
     shapes = [("4096x1M", 1 << 20, 4096), ("1024x1M", 1 << 20, 1024), ("3000x1M", 1 << 20, 3000),
               ("c2", None, None)]
+    if a.shapes:
+        shapes = [x for x in shapes if x[0] in a.shapes.split(",")]
     for name, n, L in shapes:
         if name == "c2":
             w = Workload("c2", 0, dev)
@@ -184,12 +186,13 @@ def packed_modes(a):
             offs = (torch.arange(n, dtype=torch.int64, device=dev) * L)
             lens = torch.full((n,), L, dtype=torch.int32, device=dev)
         out = torch.empty(offs.numel(), dtype=torch.int32, device=dev)
-        for path in ("rows", "packed"):
+        for path in a.paths.split(","):
             rpc_amd.set_ragged_path(path)
             f = lambda: rpc_amd.device_batch(base, offs, lens, out=out)
             ts = [timed(f, a.reps) for _ in range(a.rounds)]
             med = statistics.median(ts)
             r = {"mode": "packed", "shape": name, "path": path, "median_us": round(med * 1e6, 1),
+                 "min_slice": os.environ.get("RPCCRC_PACKED_MIN_SLICE", "default"),
                  "GiBps": round(nbytes / med / 2**30, 1)}
             res.append(r)
             print(json.dumps(r), flush=True)
@@ -281,6 +284,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--grids", default="0,512,1024")
+    ap.add_argument("--shapes", default="", help="packed mode: comma list of shapes (default all)")
+    ap.add_argument("--paths", default="rows,packed", help="packed mode: ragged paths to time")
     ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline", "packed"])
     ap.add_argument("--launches", type=int, default=60)
     ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
