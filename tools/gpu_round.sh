@@ -56,6 +56,15 @@ for s in $STEPS; do
     pmcpacked)
            run pmcpacked 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
                -d "$OUT/pmcpacked" -o run --output-format csv -- python3 tools/probe.py --mode packed --rounds 1 --reps 2 --shapes 4096x1M,1024x1M ;;
+    glob_ab)
+           for i in 1 2; do
+             RPCCRC_GLOBAL_ROUNDS=0 run ns_static$i 300 python bench.py --no-cpu-baseline --no-host-inclusive || exit 1
+             run ns_glob$i 300 python bench.py --no-cpu-baseline --no-host-inclusive || exit 1
+           done
+           RPCCRC_GLOBAL_ROUNDS=0 run c1_static 300 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive || exit 1
+           run c1_glob 300 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive || exit 1
+           RPCCRC_GLOBAL_ROUNDS=0 run c2_static 300 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive || exit 1
+           run c2_glob 300 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive || exit 1 ;;
     packed) run packed 600 python tools/probe.py --mode packed --rounds 3 --reps 5 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
