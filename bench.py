@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--nontemporal", type=int, default=-1, help="-1 = library default")
     p.add_argument("--ragged-path", default="auto", choices=["auto", "rows", "packed"],
                    help="ragged-batch kernel (C2): auto = rows for device batches; packed = 1 KiB chunks four per row")
+    p.add_argument("--chunk-kib", type=int, default=0, help="C4: chunk size (0 = library default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
@@ -65,9 +66,10 @@ def parse():
 
 
 class Workload:
-    def __init__(self, cfg: str, rank: int, device):
+    def __init__(self, cfg: str, rank: int, device, chunk: int = 0):
         desc, kind, n, L, seed = CONFIGS[cfg]
         self.name, self.desc, self.kind, self.n, self.L = cfg, desc, kind, n, L
+        self.chunk = chunk
         self.seed = rank_seed(seed, rank)
         self.device = device
         if kind == "uniform":
@@ -100,7 +102,7 @@ class Workload:
         elif self.kind == "ragged":
             rpc_amd.device_batch(self.base, self.offs, self.lens, out=self.out)
         else:
-            rpc_amd.device_large(self.base, self.large_offs, self.large_lens, out=self.out)
+            rpc_amd.device_large(self.base, self.large_offs, self.large_lens, chunk=self.chunk, out=self.out)
 
 
 def _loguniform_lengths(n, seed, lo=64, hi=65536):
@@ -269,7 +271,7 @@ def main():
         rpc_amd.set_options(nontemporal=bool(args.nontemporal))
     rpc_amd.set_ragged_path(args.ragged_path)
 
-    w = Workload(args.config, rank, device)
+    w = Workload(args.config, rank, device, chunk=args.chunk_kib * 1024)
     stream = torch.cuda.current_stream()
     prewarm_steps = 0
     t_pw = time.perf_counter()

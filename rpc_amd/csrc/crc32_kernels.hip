@@ -39,22 +39,37 @@ __device__ __forceinline__ uint32_t dev_xpow_bytes(uint64_t nbytes, const uint32
   return r;
 }
 
-__global__ void __launch_bounds__(64) crc32_chunk_combine_kernel(CombineArgs a) {
+// One 256-thread block per body.  Advancing a partial through one chunk,
+// v -> A_chunk(v), is GF(2)-linear, so it is 4 byte-table lookups:
+// T[j][x] = A_chunk(x << 8j), built in LDS by the block.  Thread t folds a
+// contiguous run of chunks with Horner, shifts its partial to the body end,
+// and the block XORs the partials.
+constexpr uint32_t kCombineThreads = 256;
+__global__ void __launch_bounds__(kCombineThreads) crc32_chunk_combine_kernel(CombineArgs a) {
+  __shared__ uint32_t tab[4][256];
+  __shared__ uint32_t part[kCombineThreads / 64];
   const uint64_t b = blockIdx.x;
-  if (b >= a.n_bodies) return;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t xchunk = dev_xpow_bytes(a.chunk, a.x2n_bytes);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) tab[j][t] = gf2_mulmod(xchunk, t << (8 * j));
+  __syncthreads();
   const uint64_t L = a.lengths[b];
   const uint64_t first = a.chunk_first[b];
   const uint64_t nch = (L + a.chunk - 1) / a.chunk;
-  const uint64_t per = (nch + 63) / 64;
-  const uint64_t k0 = lane * per;
+  const uint64_t per = (nch + kCombineThreads - 1) / kCombineThreads;
+  const uint64_t k0 = t * per;
   const uint64_t k1 = (k0 + per < nch) ? k0 + per : nch;
-  const uint32_t xchunk = dev_xpow_bytes(a.chunk, a.x2n_bytes);
   uint32_t acc = 0;
-  for (uint64_t k = k0; k < k1; ++k) acc = gf2_mulmod(xchunk, acc) ^ a.raw[first + k];
+  for (uint64_t k = k0; k < k1; ++k)
+    acc = tab[0][acc & 255u] ^ tab[1][(acc >> 8) & 255u] ^ tab[2][(acc >> 16) & 255u] ^ tab[3][acc >> 24] ^
+          a.raw[first + k];
   if (k1 > k0 && k1 < nch) acc = gf2_mulmod(dev_xpow_bytes((nch - k1) * a.chunk, a.x2n_bytes), acc);
   for (int m = 1; m < 64; m <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, m, 64);
-  if (lane == 0) {
+  if ((t & 63u) == 0) part[t >> 6] = acc;
+  __syncthreads();
+  if (t == 0) {
+    for (uint32_t w = 1; w < kCombineThreads / 64; ++w) acc ^= part[w];
     const uint32_t init = (L == 0) ? 0xFFFFFFFFu : gf2_mulmod(dev_xpow_bytes(L, a.x2n_bytes), 0xFFFFFFFFu);
     a.out[b] = (L == 0) ? 0u : ~(init ^ acc);
   }
@@ -157,7 +172,7 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
 
 hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream) {
   if (a.n_bodies == 0) return hipSuccess;
-  hipLaunchKernelGGL(crc32_chunk_combine_kernel, dim3((unsigned)a.n_bodies), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(crc32_chunk_combine_kernel, dim3((unsigned)a.n_bodies), dim3(kCombineThreads), 0, stream, a);
   return hipGetLastError();
 }
 

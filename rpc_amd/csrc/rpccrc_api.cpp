@@ -164,7 +164,7 @@ uint32_t *stream_counter(const DeviceCtx &c, hipStream_t s) {
 }
 
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
+          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s, bool even = false) {
   ItemsArgs a;
   a.base = base;
   a.offsets = offsets;
@@ -179,7 +179,7 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   a.gshift = kRowsGroupShift;
   // Global rounds pay for ragged batches (uneven per-round work: C2 -2 to -3 %)
   // but not for equal-length ones (NS +2 to +5 %, C1 +20 %: profiles/r01t, r01u).
-  a.gctr = (g_global_rounds && offsets != nullptr && QB == 1) ? stream_counter(c, s) : nullptr;
+  a.gctr = (g_global_rounds && offsets != nullptr && QB == 1 && !even) ? stream_counter(c, s) : nullptr;
   return map_hip(launch_rows(a, QB, g_nontemporal != 0, max_blocks_for(c), s));
 }
 
@@ -276,7 +276,15 @@ thread_local PinnedStage t_large_stage;
 
 int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_offsets, const uint64_t *h_lengths,
                  uint64_t n, uint32_t *d_out, uint64_t chunk, hipStream_t s) {
-  if (chunk == 0) chunk = 1u << 20;
+  if (chunk == 0) {
+    // Default: enough chunks for the rows kernel's dynamic dealing (>= 65536
+    // tasks on 256 CUs; C4: 64 KiB chunks, measured ~5 % faster than 1 MiB
+    // chunks dealt one per wave), 16 KiB .. 1 MiB.
+    uint64_t bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) bytes += h_lengths[i];
+    chunk = 1u << 20;
+    while (chunk > (16u << 10) && bytes / chunk < 65536) chunk >>= 1;
+  }
   if (chunk % 16 != 0 || chunk > (1ull << 31)) return RPCCRC_EINVAL;
   uint64_t total = 0;
   int rc = t_large_stage.reserve(n * sizeof(BodyDesc));
@@ -312,7 +320,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
                      chunk, total, d_ioff, d_ilen, d_lens, d_firsts);
   e = hipGetLastError();
   int r = map_hip(e);
-  if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
+  if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s, /*even=*/true);
   if (r == RPCCRC_OK) {
     CombineArgs ca;
     ca.raw = d_raw;

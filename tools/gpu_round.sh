@@ -65,6 +65,16 @@ for s in $STEPS; do
            run c1_glob 300 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive || exit 1
            RPCCRC_GLOBAL_ROUNDS=0 run c2_static 300 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive || exit 1
            run c2_glob 300 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive || exit 1 ;;
+    c4_chunks)
+           for k in ${C4_CHUNKS:-0 1024 256 64 32}; do
+             run c4_chunk$k 300 python bench.py --config c4 --chunk-kib $k --no-cpu-baseline --no-host-inclusive --steps 10 || exit 1
+           done
+           RPCCRC_GLOBAL_ROUNDS=0 run c4_chunk64_static 300 python bench.py --config c4 --chunk-kib 64 --no-cpu-baseline --no-host-inclusive --steps 10 || exit 1 ;;
+    prof_c4)
+           for k in 1024 64; do
+             run prof_c4_$k 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_c4_$k" -o run --output-format csv -- \
+               python3 bench.py --config c4 --chunk-kib $k --steps 10 --warmup 3 --prewarm-s 0.2 --no-cpu-baseline --no-host-inclusive || exit 1
+           done ;;
     packed) run packed 600 python tools/probe.py --mode packed --rounds 3 --reps 5 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
