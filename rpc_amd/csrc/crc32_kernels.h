@@ -23,7 +23,6 @@ struct ItemsArgs {
   const uint32_t *tq;       // Tq[q] = A_q(0xFFFFFFFF), q = 0..4096
   uint32_t *out;            // n_items CRCs
   uint32_t gshift;          // group dealing: each wave takes 2^gshift consecutive tasks per round
-  uint32_t *gctr = nullptr; // DYN global rounds: {next round, exited waves}, zero between launches
 };
 
 struct CombineArgs {

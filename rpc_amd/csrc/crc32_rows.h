@@ -387,23 +387,8 @@ struct QuarterInfo {
 // times, tools/probe.py --mode timeline.)  Finished CRCs go to an LDS ring of
 // kDynSlots rounds; the wave completing a round stores its 32 CRCs as one
 // whole 128-B line.
-//
-// Global rounds (ItemsArgs::gctr != nullptr): the last quarter of the rounds is
-// dealt ACROSS workgroups.  Local round rnd < r_static of workgroup vb is
-// global round rnd * blocks + vb as above; each later local round takes the
-// next global round from the launch's counter gctr[0], so workgroups on a
-// faster XCD take more of the tail (measured: with static rounds the odd XCDs
-// finished 2-6 % after the even ones).  The wave that grabs a round's first
-// task fetches the global round of local round + kGidAhead (the atomic's
-// latency under a saturated memory system is many rows) and publishes it in
-// an LDS ring (kGidSlots) before it can block anywhere (its grab -> publish
-// interval is one issue()),
-// so waves waiting for a round id never wait on a wave that waits on them.
-// The last wave to exit resets gctr for the next launch on the stream.
 constexpr uint32_t kDynRound = 32;
 constexpr uint32_t kDynSlots = 4;
-constexpr uint32_t kGidAhead = 8;  // a round's global id is fetched this many local rounds early
-constexpr uint32_t kGidSlots = 32; // > kGidAhead + the rounds the CRC ring lets run ahead
 constexpr uint32_t dyn_ctl_words(int QB) { return 1 + 2 * kDynSlots + kDynSlots * kDynRound * (uint32_t)QB; }
 
 template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool DYN = false>
@@ -414,12 +399,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
   // rounds (generation), then the CRC ring (QB CRCs per task).
   __shared__ uint32_t s_ctl[DYN ? dyn_ctl_words(QB) : 1];
-  // Global rounds: [0, S) global round ids, [S, 2S) the local round each holds.
-  __shared__ uint32_t s_gid[DYN ? 2 * kGidSlots : 1];
   if constexpr (DYN) {
     if (threadIdx.x <= 2 * kDynSlots)
       s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots : 0u;
-    if (threadIdx.x < kGidSlots) s_gid[kGidSlots + threadIdx.x] = 0xFFFFFFFFu;
   }
   uint64_t t_entry = 0, t_image = 0;
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
@@ -479,81 +461,15 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if (lane == 0) c = __hip_atomic_fetch_add(&s_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return c;
   };
-  const uint64_t n_rounds = (n_tasks + kDynRound - 1) / kDynRound;
-  const uint64_t r_glob = (DYN && a.gctr != nullptr) ? (n_rounds / nblk) * 3u / 4u : 0u;
-  const uint32_t r_static = r_glob >= kGidAhead ? (uint32_t)r_glob : 0xFFFFFFFFu; // first globally dealt local round
-  const uint64_t dyn_base = (uint64_t)r_glob * nblk; // first global round dealt by gctr
-  auto dyn_round = [&](uint32_t rnd) -> uint64_t { // global round of local round rnd
-    if (rnd < r_static) return (uint64_t)rnd * nblk + vb;
-    const uint32_t slot = rnd % kGidSlots;
-    uint32_t gid = 0;
-    if (lane == 0) {
-      while (__hip_atomic_load(&s_gid[kGidSlots + slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != rnd)
-        __builtin_amdgcn_s_sleep(1);
-      gid = s_gid[slot];
-    }
-    return dyn_base + (uint32_t)__builtin_amdgcn_readfirstlane((int)gid);
-  };
-  // The wave holding counter index c (just grabbed) fetches and publishes the
-  // global round of local round c / 32 + kGidAhead if c is its round's first
-  // task (rounds r_static .. r_static + kGidAhead - 1 come from the grabs of
-  // static rounds: r_static >= kGidAhead).
-  // The fetch (global atomic) and the LDS publish are a step apart: the
-  // publish sits after the next issue(), where waiting for the atomic is
-  // vmcnt(4) (the row being computed next is older), not a stall on the row
-  // just issued.  Safe: every wave that needs this id grabbed a task kGidAhead
-  // rounds later, so the fetcher's step in between cannot wait on it (the CRC
-  // ring keeps all grabs within 4 rounds of the oldest unfinished round).
-  uint32_t gf = 0, gf_rnd = 0; // lane 0: fetched global round; its local round
-  bool gf_pending = false;
-  auto dyn_fetch = [&](uint64_t c) {
-    const uint32_t rnd = (uint32_t)(c / kDynRound) + kGidAhead;
-    if (c % kDynRound != 0u || rnd < r_static) return;
-    if (lane == 0) gf = __hip_atomic_fetch_add(a.gctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    gf_rnd = rnd;
-    gf_pending = true;
-  };
-  auto dyn_post = [&]() {
-    if (!gf_pending) return;
-    if (lane == 0) {
-      const uint32_t slot = gf_rnd % kGidSlots;
-      s_gid[slot] = gf;
-      __hip_atomic_store(&s_gid[kGidSlots + slot], gf_rnd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    gf_pending = false;
-  };
-  auto dyn_publish = [&](uint64_t c) { // fetch + publish at once (prologue)
-    dyn_fetch(c);
-    dyn_post();
-  };
-  auto dyn_task = [&](uint64_t c) -> uint64_t { return (dyn_round((uint32_t)(c / kDynRound)) * kDynRound) | (c % kDynRound); };
-  // Every wave of a global-round launch counts its exit; the last one resets
-  // the counter.  Relaxed is enough: a wave's counter atomics all returned
-  // (their results were used) before its exit atomic issues, and an acq_rel
-  // atomic here costs an L2 writeback + invalidate per wave (measured +15 %).
-  auto dyn_exit = [&]() {
-    if constexpr (DYN) {
-      if (a.gctr != nullptr && lane == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(a.gctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1u == nblk * 16u) {
-          __hip_atomic_store(a.gctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(a.gctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-  };
+  auto dyn_task = [&](uint64_t c) -> uint64_t { return (((c / kDynRound) * nblk + vb) * kDynRound) | (c % kDynRound); };
   uint64_t first_c = 0, first_task;
   if constexpr (DYN) {
     first_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)dyn_grab());
-    dyn_publish(first_c);
-    first_task = dyn_task(first_c); // round 0: static (r_static >= 1)
+    first_task = dyn_task(first_c);
   } else {
     first_task = task_of(0);
   }
-  if (first_task >= n_tasks) {
-    dyn_exit();
-    return;
-  }
+  if (first_task >= n_tasks) return;
 
   auto synth = [&](uint64_t key, u32x4 (&buf)[4]) {
 #pragma unroll
@@ -643,7 +559,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     // DYN output: CRC of the task with counter index c into the LDS ring; the
     // wave completing a round stores the round's CRCs as one whole line.
-    auto dyn_out = [&](uint64_t c, uint64_t item, uint32_t res) {
+    auto dyn_out = [&](uint64_t c, uint32_t res) {
       const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots;
       uint32_t old = 0;
@@ -655,7 +571,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      const uint64_t base = item & ~(uint64_t)(kDynRound - 1u); // the round's first task
+      const uint64_t base = ((uint64_t)rnd * nblk + vb) * kDynRound;
       const uint32_t cnt = (n_tasks - base < kDynRound) ? (uint32_t)(n_tasks - base) : kDynRound;
       if (old + 1u == cnt) { // this wave completed the round
         const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
@@ -672,7 +588,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     };
     auto compute = [&](bool valid, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
-                       uint64_t cidx, uint64_t item, u32x4 (&buf)[4]) {
+                       uint64_t cidx, u32x4 (&buf)[4]) {
       const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
       const bool last = r + 1 == nr;
       if (rs < 0 || (last && z != 0)) {
@@ -702,7 +618,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (z != 0) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
         if (mode == kModeFinal) res = ~res;
         if constexpr (DYN) {
-          if (valid) dyn_out(cidx, item, res);
+          if (valid) dyn_out(cidx, res);
         } else {
           if (valid) park(res);
         }
@@ -718,13 +634,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // wave's next item.  Invalid successors carry the wave's first item's
     // (in-range) metadata and load from `safe`; their results are dropped.
     uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
-    uint32_t pend_c = 0; // ... and its value, read after the grabbing step's issue()
-    bool grabbed = false;
-    if constexpr (DYN) {
-      pend = dyn_grab();
-      pend_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-      dyn_publish(pend_c);
-    }
+    if constexpr (DYN) pend = dyn_grab();
     uint64_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
     auto succ = [&](bool ok, uint64_t item, uint32_t r, uint32_t nr, uint64_t &s_item, uint32_t &s_r,
                     bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr,
@@ -735,10 +645,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           s_item = item;
           m_c = c_c;
         } else {
-          m_c = pend_c;
+          m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
           s_item = dyn_task(m_c);
-          grabbed = ok && s_item < n;
-          if (grabbed) pend = dyn_grab(); // no more grabs once the wave is done
+          if (ok && s_item < n) pend = dyn_grab(); // no more grabs once the wave is done
         }
       } else {
         s_item = adv ? item : next_task(item);
@@ -763,15 +672,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         bool m_ok;
         succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
-        if constexpr (DYN) {
-          dyn_post(); // the previous step's fetch
-          if (grabbed) {
-            pend_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-            dyn_fetch(pend_c);
-            grabbed = false;
-          }
-        }
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, cb);
         c_c = m_c;
         c_ok = m_ok;
         c_seed = m_seed;
@@ -802,7 +703,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         bool m_ok;
         succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, c_item, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, cb);
         c_ok = n_ok;
         c_seed = n_seed;
         n_seed = m_seed;
@@ -910,7 +811,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint64_t j0 = 0;
     // DYN output (see QB = 1): the 4 CRCs of group task c into the LDS ring; the
     // wave completing a round stores its (up to) 128 CRCs as two 256-B stores.
-    auto dyn_out4 = [&](uint64_t c, uint64_t grp, const uint32_t (&v)[4]) {
+    auto dyn_out4 = [&](uint64_t c, const uint32_t (&v)[4]) {
       constexpr uint32_t kW = kDynRound * 4;
       const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots + slot * kW;
@@ -923,7 +824,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      const uint64_t base = grp & ~(uint64_t)(kDynRound - 1u); // first group of the round
+      const uint64_t base = ((uint64_t)rnd * nblk + vb) * kDynRound; // first group of the round
       const uint32_t cnt = (ngroups - base < kDynRound) ? (uint32_t)(ngroups - base) : kDynRound;
       if (old + 1u == cnt) {
         const uint64_t ibase = 4 * base;
@@ -944,7 +845,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       j0 += ocount / 4u;
       ocount = 0;
     };
-    auto compute = [&](const QuadMeta &qm, uint64_t cidx, uint64_t grp, u32x4 (&buf)[4]) {
+    auto compute = [&](const QuadMeta &qm, uint64_t cidx, u32x4 (&buf)[4]) {
       uint32_t zl = 0, zany = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -971,7 +872,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         vals[b] = v;
       }
       if constexpr (DYN) {
-        dyn_out4(cidx, grp, vals);
+        dyn_out4(cidx, vals);
       } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) outv = (lane == ocount + (uint32_t)b) ? vals[b] : outv;
@@ -984,17 +885,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       QuadMeta c_qm = issue(g, true, safe, bufA);
-      uint32_t pend = 0, pend_c = 0; // see QB = 1
-      if constexpr (DYN) {
-        pend = dyn_grab();
-        pend_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-        dyn_publish(pend_c);
-      }
+      uint32_t pend = 0;
+      if constexpr (DYN) pend = dyn_grab();
       uint64_t c_c = first_c;
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
         uint64_t ng, n_c = 0;
         if constexpr (DYN) {
-          n_c = pend_c;
+          n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
           ng = dyn_task(n_c);
         } else {
           ng = next_task(g);
@@ -1003,14 +900,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if constexpr (DYN)
           if (ok) pend = dyn_grab();
         const QuadMeta n_qm = issue(ok ? ng : g, ok, safe, nb);
-        if constexpr (DYN) {
-          dyn_post(); // the previous step's fetch
-          if (ok) {
-            pend_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-            dyn_fetch(pend_c);
-          }
-        }
-        compute(c_qm, c_c, g, cb);
+        compute(c_qm, c_c, cb);
         c_qm = n_qm;
         g = ng;
         c_c = n_c;
@@ -1029,7 +919,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         const uint64_t g2 = next_task(gn);
         const bool ok2 = g2 < ngroups;
         const QuadMeta m_qm = issue(ok2 ? g2 : g, ok2, safe, fb);
-        compute(c_qm, 0, g, cb);
+        compute(c_qm, 0, cb);
         c_qm = n_qm;
         n_qm = m_qm;
         g = gn;
@@ -1054,8 +944,6 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     }
   }
-  if constexpr (DYN) dyn_post();
-  dyn_exit();
 }
 
 } // namespace rpccrc

@@ -37,13 +37,7 @@ struct DeviceCtx {
   int status = RPCCRC_ENODEV;
   char name[128] = {0};
   char arch[64] = {0};
-  // Rows-kernel global-round counters (crc32_rows.h kGidSlots), one pair per
-  // stream: launches on one stream run in order and each leaves its pair zeroed.
-  mutable std::mutex ctr_mu;
-  mutable uint32_t *ctr_slab = nullptr;
-  mutable std::vector<hipStream_t> ctr_streams;
 };
-constexpr size_t kCtrSlab = 512; // counter pairs per device (more streams: static dealing)
 
 DeviceCtx g_dev[kMaxDevices];
 std::once_flag g_once[kMaxDevices];
@@ -51,12 +45,6 @@ std::once_flag g_once[kMaxDevices];
 int g_nontemporal = 1; // streamed once: non-temporal loads (measured faster)
 int g_max_blocks = 0;
 int g_ragged_path = RPCCRC_RAGGED_AUTO;
-// Cross-workgroup dealing of the rows kernel's last rounds for ragged batches
-// (DESIGN.md 4.1).  Tuning override: RPCCRC_GLOBAL_ROUNDS=0 keeps every round static.
-const bool g_global_rounds = [] {
-  const char *e = getenv("RPCCRC_GLOBAL_ROUNDS");
-  return !(e && e[0] == '0');
-}();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kPackedMinBodies = 64;         // fewer bodies: one wave per body (rows kernel)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
@@ -122,13 +110,6 @@ void init_device(int dev) {
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.x2n, x2n.data(), 64 * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess && hipMalloc(&c.ctr_slab, kCtrSlab * 8) == hipSuccess) { // else: static dealing only
-    std::vector<uint32_t> zero(kCtrSlab * 2, 0u);
-    if (hipMemcpy(c.ctr_slab, zero.data(), kCtrSlab * 8, hipMemcpyHostToDevice) != hipSuccess) {
-      (void)hipFree(c.ctr_slab);
-      c.ctr_slab = nullptr;
-    }
-  }
   (void)hipSetDevice(prev);
   c.status = map_hip(e);
 }
@@ -151,20 +132,8 @@ int max_blocks_for(const DeviceCtx &c) {
   return mb;
 }
 
-// The zeroed counter pair of stream s, or nullptr (the per-thread default
-// stream is a different stream in every thread; slab exhausted).
-uint32_t *stream_counter(const DeviceCtx &c, hipStream_t s) {
-  if (s == hipStreamPerThread) return nullptr;
-  std::lock_guard<std::mutex> lock(c.ctr_mu);
-  for (size_t i = 0; i < c.ctr_streams.size(); ++i)
-    if (c.ctr_streams[i] == s) return c.ctr_slab + 2 * i;
-  if (c.ctr_slab == nullptr || c.ctr_streams.size() >= kCtrSlab) return nullptr;
-  c.ctr_streams.push_back(s);
-  return c.ctr_slab + 2 * (c.ctr_streams.size() - 1);
-}
-
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s, bool even = false) {
+          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
   ItemsArgs a;
   a.base = base;
   a.offsets = offsets;
@@ -177,9 +146,6 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   a.tq = c.tq;
   a.out = out;
   a.gshift = kRowsGroupShift;
-  // Global rounds pay for ragged batches (uneven per-round work: C2 -2 to -3 %)
-  // but not for equal-length ones (NS +2 to +5 %, C1 +20 %: profiles/r01t, r01u).
-  a.gctr = (g_global_rounds && offsets != nullptr && QB == 1 && !even) ? stream_counter(c, s) : nullptr;
   return map_hip(launch_rows(a, QB, g_nontemporal != 0, max_blocks_for(c), s));
 }
 
@@ -320,7 +286,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
                      chunk, total, d_ioff, d_ilen, d_lens, d_firsts);
   e = hipGetLastError();
   int r = map_hip(e);
-  if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s, /*even=*/true);
+  if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
   if (r == RPCCRC_OK) {
     CombineArgs ca;
     ca.raw = d_raw;

@@ -1,0 +1,24 @@
+#!/bin/bash
+# tools/ab_lib.sh -- interleaved A/B of librpccrc builds on one box.
+# Usage: bash tools/ab_lib.sh TAG "libA libB ..." "cfg1 cfg2 ..." [rounds]
+# lib "head" = the in-tree library; other names = abtest/<name>.so.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=$1; LIBS=$2; CFGS=$3; ROUNDS=${4:-2}
+OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+for i in $(seq 1 "$ROUNDS"); do
+  for c in $CFGS; do
+    for l in $LIBS; do
+      if [ "$l" = head ]; then unset RPCCRC_LIB; else export RPCCRC_LIB=$PWD/abtest/$l.so; fi
+      timeout -k 10 300 python bench.py --config "$c" --no-cpu-baseline --no-host-inclusive > "$OUT/${c}_${l}_$i.log" 2>&1
+      rc=$?
+      if [ $rc -ne 0 ]; then echo "FAIL $c $l rc=$rc"; tail -3 "$OUT/${c}_${l}_$i.log"; [ $rc -ge 124 ] && exit $rc; continue; fi
+      python3 - "$OUT/${c}_${l}_$i.log" "$c" "$l" <<'PY'
+import json, sys
+line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
+d = json.loads(line)
+print(sys.argv[2], sys.argv[3], d["roofline"]["avg_launch_us"], d["roofline"]["frac"])
+PY
+    done
+  done
+done | tee "$OUT/ab.txt"

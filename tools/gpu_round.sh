@@ -56,20 +56,10 @@ for s in $STEPS; do
     pmcpacked)
            run pmcpacked 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
                -d "$OUT/pmcpacked" -o run --output-format csv -- python3 tools/probe.py --mode packed --rounds 1 --reps 2 --shapes 4096x1M,1024x1M ;;
-    glob_ab)
-           for i in 1 2; do
-             RPCCRC_GLOBAL_ROUNDS=0 run ns_static$i 300 python bench.py --no-cpu-baseline --no-host-inclusive || exit 1
-             run ns_glob$i 300 python bench.py --no-cpu-baseline --no-host-inclusive || exit 1
-           done
-           RPCCRC_GLOBAL_ROUNDS=0 run c1_static 300 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive || exit 1
-           run c1_glob 300 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive || exit 1
-           RPCCRC_GLOBAL_ROUNDS=0 run c2_static 300 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive || exit 1
-           run c2_glob 300 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive || exit 1 ;;
     c4_chunks)
            for k in ${C4_CHUNKS:-0 1024 256 64 32}; do
              run c4_chunk$k 300 python bench.py --config c4 --chunk-kib $k --no-cpu-baseline --no-host-inclusive --steps 10 || exit 1
-           done
-           RPCCRC_GLOBAL_ROUNDS=0 run c4_chunk64_static 300 python bench.py --config c4 --chunk-kib 64 --no-cpu-baseline --no-host-inclusive --steps 10 || exit 1 ;;
+           done ;;
     prof_c4)
            for k in 1024 64; do
              run prof_c4_$k 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_c4_$k" -o run --output-format csv -- \
