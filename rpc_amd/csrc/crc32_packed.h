@@ -345,8 +345,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const uint32_t clen = q_clen(q[b].info), z = q_z(q[b].info);
-      const int32_t vstart = (int32_t)(clen + z) - (int32_t)kChunk;
-      if (vstart < 0 || z != 0u) buf[b] = mask_piece32(buf[b], vstart + (int32_t)pofs, (int32_t)clen);
+      // the quarter's first real byte sits at window offset kChunk - clen - z
+      fix_quarter(buf[b], lane, kChunk - clen - z, z);
       const bool seeded = (q[b].info & kQFirst) != 0u && mode != kModeRaw;
       const uint32_t seed = seeded ? (uint32_t)__builtin_amdgcn_readlane((int)seedv, q[b].lane) : 0u;
       sl = (hi == (uint32_t)b) ? seed : sl;

@@ -89,3 +89,15 @@ def test_emulated_packed_kernel_matches_oracle(rows_emu, mis, nwaves, min_slice,
     for i, (L, o) in enumerate(zip(lens, out)):
         assert int(o, 16) == oracle.crc32(data[off:off + L]), (i, mis, L)
         off += L
+
+
+def test_edge_fix_matches_byte_mask(tmp_path):
+    """The kernels' edge fix (crc32_edge.h masks on the two edge pieces of a
+    window) equals a per-byte mask of the whole window, for every front offset
+    and pad z (tests/cpu_emu/edge_emu.cpp)."""
+    exe = str(tmp_path / "edge_emu")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(REPO, "tests/cpu_emu/edge_emu.cpp")],
+                   check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok ")

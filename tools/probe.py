@@ -26,7 +26,12 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import rpc_amd  # noqa: E402
+import bench  # noqa: E402
 from bench import Workload  # noqa: E402
+
+# probe-only uniform shapes: bodies shorter than a 4 KiB row (every row partial)
+bench.CONFIGS.setdefault("u3k", ("probe: 1M x 3 KiB equal-length bodies", "uniform", 1 << 20, 3072, 0x5EED0103))
+bench.CONFIGS.setdefault("u2k", ("probe: 2M x 2 KiB equal-length bodies", "uniform", 1 << 21, 2048, 0x5EED0102))
 
 
 def timed(fn, reps):
