@@ -32,7 +32,8 @@ struct CombineArgs {
   const uint32_t *x2n_bytes;    // x^(8*2^k) mod P, k = 0..63
   uint64_t n_bodies;
   uint64_t chunk;               // chunk size in bytes (multiple of 16)
-  uint32_t *out;
+  uint32_t *out;                // zeroed before the launch: blocks XOR their partials in
+  uint32_t splits = 1;          // blocks per body (each folds a contiguous run of chunks)
 };
 
 // QB = 1: rows of 4 KiB of one item (any length); QB = 4: four items per row,

@@ -9,7 +9,7 @@
 //    across rows; QB = 4: four <= 1 KiB bodies per row).  Coalesced 16-B
 //    non-temporal loads, permlane transpose, slice-by-4 lookups, GF(2) merge.
 //  * crc32_chunk_combine_kernel (below): folds chunk CRCs of large bodies
-//    (zlib crc32_combine algebra), one wave per body.
+//    (zlib crc32_combine algebra), several blocks per body.
 //  * splitmix_fill_kernel / stream_read_kernel: synthetic data and the
 //    achievable-HBM-read probe used by bench.py.
 //  No MFMA: this is a byte scan.
@@ -29,7 +29,7 @@ namespace rpccrc {
 // ---------------------------------------------------------------------------
 // Chunk combine for large bodies: body b's chunk CRCs raw[cfirst[b] + k],
 // k = 0..nch-1 (end-aligned chunks of `chunk` bytes, all crc0) are folded into
-// crc(body) = ~(A_L(F) ^ XOR_k A_{(nch-1-k)*chunk}(raw_k)).  One wave per body.
+// crc(body) = ~(A_L(F) ^ XOR_k A_{(nch-1-k)*chunk}(raw_k)).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t dev_xpow_bytes(uint64_t nbytes, const uint32_t *x2n_bytes) {
   // x2n_bytes[k] = x^(8 * 2^k) mod P, k = 0..63.
@@ -39,27 +39,35 @@ __device__ __forceinline__ uint32_t dev_xpow_bytes(uint64_t nbytes, const uint32
   return r;
 }
 
-// One 256-thread block per body.  Advancing a partial through one chunk,
-// v -> A_chunk(v), is GF(2)-linear, so it is 4 byte-table lookups:
-// T[j][x] = A_chunk(x << 8j), built in LDS by the block.  Thread t folds a
-// contiguous run of chunks with Horner, shifts its partial to the body end,
-// and the block XORs the partials.
+// `splits` 256-thread blocks per body; block s folds a contiguous run of the
+// body's chunks.  Advancing a partial through one chunk, v -> A_chunk(v), is
+// GF(2)-linear, so it is 4 byte-table lookups: T[j][x] = A_chunk(x << 8j),
+// built in LDS by the block.  Thread t folds its run with Horner and shifts
+// the partial to the body end; the block XORs its threads' partials and
+// atomically XORs the sum into out[b] (zeroed beforehand; block 0 adds the
+// ~A_L(0xFFFFFFFF) term, so out[b] ends as ~(A_L(F) ^ XOR_k ...)).  Several
+// blocks per body keep the chip busy with small chunks (1M chunks of 4 KiB
+// for C4: 16 blocks folding 65536 partials each took tens of microseconds).
 constexpr uint32_t kCombineThreads = 256;
 __global__ void __launch_bounds__(kCombineThreads) crc32_chunk_combine_kernel(CombineArgs a) {
   __shared__ uint32_t tab[4][256];
   __shared__ uint32_t part[kCombineThreads / 64];
-  const uint64_t b = blockIdx.x;
+  const uint64_t b = blockIdx.x / a.splits;
+  const uint32_t s = blockIdx.x % a.splits;
   const uint32_t t = threadIdx.x;
+  const uint64_t L = a.lengths[b];
+  const uint64_t first = a.chunk_first[b];
+  const uint64_t nch = (L + a.chunk - 1) / a.chunk;
+  const uint64_t pb = (nch + a.splits - 1) / a.splits;
+  const uint64_t c0 = s * pb, c1 = (c0 + pb < nch) ? c0 + pb : nch;
+  if (c0 >= c1) return; // (block-uniform) no chunks here; empty bodies stay 0
   const uint32_t xchunk = dev_xpow_bytes(a.chunk, a.x2n_bytes);
 #pragma unroll
   for (int j = 0; j < 4; ++j) tab[j][t] = gf2_mulmod(xchunk, t << (8 * j));
   __syncthreads();
-  const uint64_t L = a.lengths[b];
-  const uint64_t first = a.chunk_first[b];
-  const uint64_t nch = (L + a.chunk - 1) / a.chunk;
-  const uint64_t per = (nch + kCombineThreads - 1) / kCombineThreads;
-  const uint64_t k0 = t * per;
-  const uint64_t k1 = (k0 + per < nch) ? k0 + per : nch;
+  const uint64_t per = (c1 - c0 + kCombineThreads - 1) / kCombineThreads;
+  const uint64_t k0 = c0 + t * per;
+  const uint64_t k1 = (k0 + per < c1) ? k0 + per : c1;
   uint32_t acc = 0;
   for (uint64_t k = k0; k < k1; ++k)
     acc = tab[0][acc & 255u] ^ tab[1][(acc >> 8) & 255u] ^ tab[2][(acc >> 16) & 255u] ^ tab[3][acc >> 24] ^
@@ -70,8 +78,8 @@ __global__ void __launch_bounds__(kCombineThreads) crc32_chunk_combine_kernel(Co
   __syncthreads();
   if (t == 0) {
     for (uint32_t w = 1; w < kCombineThreads / 64; ++w) acc ^= part[w];
-    const uint32_t init = (L == 0) ? 0xFFFFFFFFu : gf2_mulmod(dev_xpow_bytes(L, a.x2n_bytes), 0xFFFFFFFFu);
-    a.out[b] = (L == 0) ? 0u : ~(init ^ acc);
+    if (s == 0) acc ^= ~gf2_mulmod(dev_xpow_bytes(L, a.x2n_bytes), 0xFFFFFFFFu);
+    atomicXor(a.out + b, acc);
   }
 }
 
@@ -172,7 +180,9 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
 
 hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream) {
   if (a.n_bodies == 0) return hipSuccess;
-  hipLaunchKernelGGL(crc32_chunk_combine_kernel, dim3((unsigned)a.n_bodies), dim3(kCombineThreads), 0, stream, a);
+  const uint64_t blocks = a.n_bodies * a.splits;
+  if (a.splits == 0 || blocks >= (1ull << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(crc32_chunk_combine_kernel, dim3((unsigned)blocks), dim3(kCombineThreads), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -45,6 +45,15 @@ std::once_flag g_once[kMaxDevices];
 int g_nontemporal = 1; // streamed once: non-temporal loads (measured faster)
 int g_max_blocks = 0;
 int g_ragged_path = RPCCRC_RAGGED_AUTO;
+// Large-body chunk (rpc_crc32_device_large, chunk_bytes = 0).  C4 per call
+// (profiles/r01c4_*): 4 KiB 697 us (rows kernel fastest, combine 27 us),
+// 16 KiB 673 us, 64 KiB 689 us (each wave streams its own 64 KiB).
+// Tuning override: RPCCRC_LARGE_CHUNK (bytes, multiple of 16).
+const uint64_t g_large_chunk = [] {
+  const char *e = getenv("RPCCRC_LARGE_CHUNK");
+  const unsigned long long v = e ? strtoull(e, nullptr, 10) : 0ull;
+  return (v >= 16 && v % 16 == 0 && v <= (1ull << 31)) ? (uint64_t)v : (uint64_t)16384;
+}();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kPackedMinBodies = 64;         // fewer bodies: one wave per body (rows kernel)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
@@ -191,11 +200,13 @@ struct BodyDesc {
 };
 
 __global__ void expand_chunks_kernel(const BodyDesc *bodies, uint64_t nb, uint64_t chunk, uint64_t total_chunks,
-                                     uint64_t *item_off, uint32_t *item_len, uint64_t *lens, uint64_t *firsts) {
+                                     uint64_t *item_off, uint32_t *item_len, uint64_t *lens, uint64_t *firsts,
+                                     uint32_t *out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < nb) {
     lens[t] = bodies[t].len;
     firsts[t] = bodies[t].chunk_first;
+    out[t] = 0; // the combine XORs its partials in
   }
   if (t >= total_chunks) return;
   uint64_t lo = 0, hi = nb; // last body with chunk_first <= t
@@ -242,17 +253,9 @@ thread_local PinnedStage t_large_stage;
 
 int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_offsets, const uint64_t *h_lengths,
                  uint64_t n, uint32_t *d_out, uint64_t chunk, hipStream_t s) {
-  if (chunk == 0) {
-    // Default: enough chunks for the rows kernel's dynamic dealing (>= 65536
-    // tasks on 256 CUs; C4: 64 KiB chunks, measured ~5 % faster than 1 MiB
-    // chunks dealt one per wave), 16 KiB .. 1 MiB.
-    uint64_t bytes = 0;
-    for (uint64_t i = 0; i < n; ++i) bytes += h_lengths[i];
-    chunk = 1u << 20;
-    while (chunk > (16u << 10) && bytes / chunk < 65536) chunk >>= 1;
-  }
+  if (chunk == 0) chunk = g_large_chunk;
   if (chunk % 16 != 0 || chunk > (1ull << 31)) return RPCCRC_EINVAL;
-  uint64_t total = 0;
+  uint64_t total = 0, max_nch = 0;
   int rc = t_large_stage.reserve(n * sizeof(BodyDesc));
   if (rc) return rc;
   BodyDesc *bd = static_cast<BodyDesc *>(t_large_stage.ptr);
@@ -260,7 +263,9 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     bd[i].off = h_offsets[i];
     bd[i].len = h_lengths[i];
     bd[i].chunk_first = total;
-    total += (h_lengths[i] + chunk - 1) / chunk;
+    const uint64_t nch = (h_lengths[i] + chunk - 1) / chunk;
+    total += nch;
+    max_nch = std::max(max_nch, nch);
   }
   if (total == 0) { // all bodies empty
     RPCCRC_TRY(hipMemsetAsync(d_out, 0, n * 4, s));
@@ -283,7 +288,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   }
   const uint64_t threads = std::max<uint64_t>(total, n);
   hipLaunchKernelGGL(expand_chunks_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, d_bodies, n,
-                     chunk, total, d_ioff, d_ilen, d_lens, d_firsts);
+                     chunk, total, d_ioff, d_ilen, d_lens, d_firsts, d_out);
   e = hipGetLastError();
   int r = map_hip(e);
   if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
@@ -296,6 +301,10 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     ca.n_bodies = n;
     ca.chunk = chunk;
     ca.out = d_out;
+    // blocks per body: about 1024 chunks each, at most 2^20 blocks in all
+    uint64_t sp = (max_nch + 1023) / 1024;
+    sp = std::max<uint64_t>(1, std::min<uint64_t>(sp, (1ull << 20) / n));
+    ca.splits = (uint32_t)sp;
     r = map_hip(launch_chunk_combine(ca, s));
   }
   (void)hipFreeAsync(ws, s);

@@ -245,7 +245,7 @@ def test_device_json_c0(golden):
     assert got[:16].tolist() == golden["json_c0"]["crcs"]
 
 
-@pytest.mark.parametrize("chunk", [0, 65536, 4096 + 16])
+@pytest.mark.parametrize("chunk", [0, 1024, 65536, 4096 + 16])
 def test_device_large(chunk):
     lens = [0, 1, 17, 4096, (5 << 20) + 3, (33 << 20) + 11]
     offs, pos = [], 5

@@ -61,7 +61,7 @@ for s in $STEPS; do
              run c4_chunk$k 300 python bench.py --config c4 --chunk-kib $k --no-cpu-baseline --no-host-inclusive --steps 10 || exit 1
            done ;;
     prof_c4)
-           for k in 1024 64; do
+           for k in ${C4_PROF_CHUNKS:-1024 64}; do
              run prof_c4_$k 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_c4_$k" -o run --output-format csv -- \
                python3 bench.py --config c4 --chunk-kib $k --steps 10 --warmup 3 --prewarm-s 0.2 --no-cpu-baseline --no-host-inclusive || exit 1
            done ;;
