@@ -206,6 +206,42 @@ def packed_modes(a):
         torch.cuda.empty_cache()
 
 
+def stream_rows(a):
+    """Row-shape stream probes (tools/probe_kernels.hip stream_rows_probe): per
+    mode, GB/s and tiles (wave iterations) per us over the north-star buffer,
+    after a clock prewarm, interleaved rounds."""
+    import time
+    so = os.path.join(REPO, "tools", "libprobe.so")
+    lib = ctypes.CDLL(so)
+    lib.probe_stream_rows.restype = ctypes.c_int
+    lib.probe_stream_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.c_void_p]
+    w = Workload("ns", 0, torch.device("cuda", 0))
+    out = torch.empty(16, dtype=torch.int32, device=w.device)
+    s = torch.cuda.current_stream()
+    tb = {0: 4096, 1: 3072, 2: 3072, 3: 8192}
+    names = {0: "4 loads / 4 KiB", 1: "3 loads + 1 out-of-range / 3 KiB", 2: "3 loads / 3 KiB", 3: "8 loads / 8 KiB"}
+
+    def mk(m):
+        def f():
+            assert lib.probe_stream_rows(w.base.data_ptr(), w.total, m, 256, out.data_ptr(), s.cuda_stream) == 0
+        return f
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        mk(0)()
+    torch.cuda.synchronize()
+    res = {m: [] for m in tb}
+    for _ in range(a.rounds):
+        for m in tb:
+            res[m].append(timed(mk(m), a.reps))
+    for m, ts in res.items():
+        med = statistics.median(ts)
+        tiles = w.total // tb[m]
+        nb = tiles * tb[m]
+        print(json.dumps({"mode": "streamrows", "variant": m, "shape": names[m], "median_us": round(med * 1e6, 1),
+                          "GBps": round(nb / med / 1e9, 1), "tiles_per_us": round(tiles / med / 1e6, 1)}), flush=True)
+
+
 def sample_smi(stop, log):
     """Child-process power/clock sampler (best effort; rocm-smi or amd-smi)."""
     import threading  # noqa: F401
@@ -291,7 +327,7 @@ def main():
     ap.add_argument("--grids", default="0,512,1024")
     ap.add_argument("--shapes", default="", help="packed mode: comma list of shapes (default all)")
     ap.add_argument("--paths", default="rows,packed", help="packed mode: ragged paths to time")
-    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline", "packed"])
+    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline", "packed", "streamrows"])
     ap.add_argument("--launches", type=int, default=60)
     ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
@@ -302,6 +338,8 @@ def main():
     torch.cuda.set_device(0)
     if a.mode == "packed":
         return packed_modes(a)
+    if a.mode == "streamrows":
+        return stream_rows(a)
     w = Workload(a.config, 0, torch.device("cuda", 0))
     if a.mode == "sustain":
         return sustain(w, a)

@@ -78,3 +78,48 @@ extern "C" __attribute__((visibility("default"))) int probe_rows(const uint8_t *
   return probe_rows_times(d_base, n, len, stride, d_out, qb, pair, nt, abl, depth, blocks, stream, nullptr,
                           pair >> 8);
 }
+
+// ---------------------------------------------------------------------------
+// Row-shape stream probes (MEASUREMENT ONLY): does a wave-iteration cost track
+// the bytes it reads or the load instructions it issues?  Tile t of TB bytes
+// (t = gw + k * nwaves, all waves one moving window), NT buffer loads of 1 KiB
+// per instruction (lane L at 16 L):
+//   MODE 0: 4 loads, TB = 4 KiB          MODE 1: 3 loads + 1 out-of-range, TB = 3 KiB
+//   MODE 2: 3 loads, TB = 3 KiB          MODE 3: 8 loads, TB = 8 KiB
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ void __launch_bounds__(1024, 4) stream_rows_probe(const uint8_t *p, uint64_t ntiles, uint32_t *out) {
+  constexpr uint32_t TB = MODE == 0 ? 4096 : MODE == 3 ? 8192 : 3072;
+  constexpr int NL = MODE == 3 ? 8 : MODE == 2 ? 3 : 4;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t gw = (uint64_t)blockIdx.x * 16u + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 16u;
+  uint32_t acc = 0;
+  for (uint64_t t = gw; t < ntiles; t += nw) {
+    const auto rs = rows::row_rsrc((uint64_t)(uintptr_t)(p + t * TB));
+    rows::u32x4 v[NL];
+#pragma unroll
+    for (int b = 0; b < NL; ++b) {
+      const uint32_t off = (MODE == 1 && b == 3) ? rows::kOobOffset : (uint32_t)(b * 1024 + 16 * lane);
+      v[b] = rows::ldb16<true>(rs, off);
+    }
+#pragma unroll
+    for (int b = 0; b < NL; ++b) acc ^= v[b][0] ^ v[b][1] ^ v[b][2] ^ v[b][3];
+  }
+  if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+extern "C" __attribute__((visibility("default"))) int probe_stream_rows(const uint8_t *d_base, uint64_t nbytes, int mode,
+                                                                         int blocks, uint32_t *d_out, void *stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint64_t tb = mode == 0 ? 4096 : mode == 3 ? 8192 : 3072;
+  const uint64_t nt = nbytes / tb;
+  switch (mode) {
+  case 0: hipLaunchKernelGGL(stream_rows_probe<0>, dim3(blocks), dim3(1024), 0, s, d_base, nt, d_out); break;
+  case 1: hipLaunchKernelGGL(stream_rows_probe<1>, dim3(blocks), dim3(1024), 0, s, d_base, nt, d_out); break;
+  case 2: hipLaunchKernelGGL(stream_rows_probe<2>, dim3(blocks), dim3(1024), 0, s, d_base, nt, d_out); break;
+  case 3: hipLaunchKernelGGL(stream_rows_probe<3>, dim3(blocks), dim3(1024), 0, s, d_base, nt, d_out); break;
+  default: return -22;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
