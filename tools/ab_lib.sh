@@ -1,7 +1,8 @@
 #!/bin/bash
 # tools/ab_lib.sh -- interleaved A/B of librpccrc builds on one box.
 # Usage: bash tools/ab_lib.sh TAG "libA libB ..." "cfg1 cfg2 ..." [rounds]
-# lib "head" = the in-tree library; other names = abtest/<name>.so.
+# lib "head" = the in-tree library; other names = abtest/<name>.so; a lib may
+# carry environment settings after a colon, commas for spaces: head:RPCCRC_X=0
 # cfg may carry bench flags after a colon, commas for spaces: c4:--chunk-kib,4
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -10,13 +11,14 @@ OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 for i in $(seq 1 "$ROUNDS"); do
   for c in $CFGS; do
     for l in $LIBS; do
-      if [ "$l" = head ]; then unset RPCCRC_LIB; else export RPCCRC_LIB=$PWD/abtest/$l.so; fi
+      lib=${l%%:*}; envs=""; [ "$lib" != "$l" ] && envs=$(echo "${l#*:}" | tr ',' ' ')
+      if [ "$lib" = head ]; then unset RPCCRC_LIB; else export RPCCRC_LIB=$PWD/abtest/$lib.so; fi
       cfg=${c%%:*}; extra=""; [ "$cfg" != "$c" ] && extra=$(echo "${c#*:}" | tr ',' ' ')
-      tag=$(echo "$c" | tr -c 'a-zA-Z0-9_\n' '_')
-      timeout -k 10 300 python bench.py --config "$cfg" $extra --no-cpu-baseline --no-host-inclusive > "$OUT/${tag}_${l}_$i.log" 2>&1
+      tag=$(echo "$c" | tr -c 'a-zA-Z0-9_\n' '_'); ltag=$(echo "$l" | tr -c 'a-zA-Z0-9_\n' '_')
+      timeout -k 10 300 env $envs python bench.py --config "$cfg" $extra --no-cpu-baseline --no-host-inclusive > "$OUT/${tag}_${ltag}_$i.log" 2>&1
       rc=$?
-      if [ $rc -ne 0 ]; then echo "FAIL $c $l rc=$rc"; tail -3 "$OUT/${tag}_${l}_$i.log"; [ $rc -ge 124 ] && exit $rc; continue; fi
-      python3 - "$OUT/${tag}_${l}_$i.log" "$c" "$l" <<'PY'
+      if [ $rc -ne 0 ]; then echo "FAIL $c $l rc=$rc"; tail -3 "$OUT/${tag}_${ltag}_$i.log"; [ $rc -ge 124 ] && exit $rc; continue; fi
+      python3 - "$OUT/${tag}_${ltag}_$i.log" "$c" "$l" <<'PY'
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
 d = json.loads(line)
