@@ -842,7 +842,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       j0 += ocount / 4u;
       ocount = 0;
     };
-    auto compute = [&](const QuadMeta &qm, uint64_t cidx, u32x4 (&buf)[4]) {
+    auto compute = [&](const QuadMeta &qm, bool valid, uint64_t cidx, u32x4 (&buf)[4]) {
       uint32_t zl = 0, zany = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -869,6 +869,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if ((qm.lz[b] >> 4) == 0) v = 0u;
         vals[b] = v;
       }
+      if (!valid) return; // a trailing step past the wave's last group
       if constexpr (DYN) {
         dyn_out4(cidx, vals);
       } else {
@@ -886,7 +887,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       uint32_t pend = 0;
       if constexpr (DYN) pend = dyn_grab();
       uint64_t c_c = first_c;
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) -> bool {
+      bool c_ok = true; // the group being computed next is real
+      // One exit, at the bottom (see QB = 1): a mid-body break made the
+      // compiler drain vmcnt before the next group's loads on every step
+      // (ISA: s_waitcnt vmcnt(0) ahead of the offset of the 4th quarter load).
+      // Steps past the wave's last group load nothing and store nothing.
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
         uint64_t ng, n_c = 0;
         if constexpr (DYN) {
           n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
@@ -894,20 +900,20 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         } else {
           ng = next_task(g);
         }
-        const bool ok = ng < ngroups;
+        const bool ok = c_ok && ng < ngroups;
         if constexpr (DYN)
           if (ok) pend = dyn_grab();
         const QuadMeta n_qm = issue(ok ? ng : g, ok, safe, nb);
-        compute(c_qm, c_c, cb);
+        compute(c_qm, c_ok, c_c, cb);
         c_qm = n_qm;
-        g = ng;
+        g = ok ? ng : g;
         c_c = n_c;
-        return ok;
+        c_ok = ok;
       };
-      for (;;) {
-        if (!step(bufA, bufB)) break;
-        if (!step(bufB, bufA)) break;
-      }
+      do {
+        step(bufA, bufB);
+        step(bufB, bufA);
+      } while (c_ok);
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
@@ -917,7 +923,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         const uint64_t g2 = next_task(gn);
         const bool ok2 = g2 < ngroups;
         const QuadMeta m_qm = issue(ok2 ? g2 : g, ok2, safe, fb);
-        compute(c_qm, 0, cb);
+        compute(c_qm, true, 0, cb);
         c_qm = n_qm;
         n_qm = m_qm;
         g = gn;
