@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="ns", choices=sorted(CONFIGS))
     p.add_argument("--nontemporal", type=int, default=-1, help="-1 = library default")
-    p.add_argument("--ragged-path", default="auto", choices=["auto", "rows", "packed"],
+    p.add_argument("--ragged-path", default="auto", choices=["auto", "rows", "packed", "split"],
                    help="ragged-batch kernel (C2): auto = rows for device batches; packed = 1 KiB chunks four per row")
     p.add_argument("--chunk-kib", type=int, default=0, help="C4: chunk size (0 = library default)")
     p.add_argument("--no-cpu-baseline", action="store_true")

@@ -170,15 +170,18 @@ RPCCRC_API int rpc_crc32_set_options(int nontemporal, int max_blocks);
 
 /* Kernel for ragged device batches (process-wide; used by rpc_crc32_device_batch,
  * rpc_crc32_batch and the frames calls).  Results are identical either way.
- *   RPCCRC_RAGGED_AUTO   frames calls (bodies <= MAX_BODY_LEN): packed for
- *                        n >= 64; other batches: rows (default)
+ *   RPCCRC_RAGGED_AUTO   frames calls (bodies <= MAX_BODY_LEN): split;
+ *                        other batches: rows (default)
  *   RPCCRC_RAGGED_ROWS   one wavefront per body, 4 KiB rows
  *   RPCCRC_RAGGED_PACKED 1 KiB chunks of consecutive bodies packed four per
  *                        row, balanced by chunk count
+ *   RPCCRC_RAGGED_SPLIT  bodies of <= 1 KiB (with their 16-B end pad) four per
+ *                        row, the rest one wavefront per body
  * Returns RPCCRC_EINVAL for any other value. */
 #define RPCCRC_RAGGED_AUTO 0
 #define RPCCRC_RAGGED_ROWS 1
 #define RPCCRC_RAGGED_PACKED 2
+#define RPCCRC_RAGGED_SPLIT 3
 RPCCRC_API int rpc_crc32_set_ragged_path(int path);
 
 /* Human-readable text for a negative return code. */

@@ -221,13 +221,14 @@ def set_options(nontemporal: bool = False, max_blocks: int = 0):
 
 
 #: rpc_crc32_set_ragged_path codes (include/rpccrc.h RPCCRC_RAGGED_*)
-RAGGED_PATHS = {"auto": 0, "rows": 1, "packed": 2}
+RAGGED_PATHS = {"auto": 0, "rows": 1, "packed": 2, "split": 3}
 
 
 def set_ragged_path(path="auto"):
     """Kernel for ragged device batches: "auto" (frames: packed, other batches: rows),
-    "rows" (one wavefront per body) or "packed" (1 KiB chunks of consecutive
-    bodies, four per row)."""
+    "rows" (one wavefront per body), "packed" (1 KiB chunks of consecutive
+    bodies, four per row) or "split" (bodies <= 1 KiB four per row, the rest
+    one wavefront per body)."""
     code = RAGGED_PATHS[path] if isinstance(path, str) else int(path)
     check(_lib.rpc_crc32_set_ragged_path(code), "rpc_crc32_set_ragged_path")
 

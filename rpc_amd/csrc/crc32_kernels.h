@@ -23,6 +23,11 @@ struct ItemsArgs {
   const uint32_t *tq;       // Tq[q] = A_q(0xFFFFFFFF), q = 0..4096
   uint32_t *out;            // n_items CRCs
   uint32_t gshift;          // group dealing: each wave takes 2^gshift consecutive tasks per round
+  // Split ragged batches (launch_split_batch): the item count is read on the
+  // device (n_items is then only the upper bound the grid is sized for) and
+  // item i's CRC goes to out[out_idx[i]].
+  const uint64_t *n_dev = nullptr;
+  const uint32_t *out_idx = nullptr;
 };
 
 struct CombineArgs {
@@ -61,6 +66,18 @@ struct PackedBatch {
 };
 hipError_t packed_workspace_bytes(uint64_t n, uint64_t max_slices, size_t *bytes);
 hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hipStream_t stream);
+// Split ragged batches (crc32_kernels.hip): small bodies (len + end pad <= 1 KiB)
+// through the QB = 4 rows kernel, the rest through QB = 1; n < 2^32 - 1.  proto
+// carries the batch (offsets / lengths required); ws must hold
+// split_workspace_bytes(n) bytes of device memory, stream-ordered with the launch.
+struct SplitLists {
+  uint64_t *counts; // [small, big]
+  uint64_t *s_off, *b_off;
+  uint32_t *s_len, *s_idx, *b_len, *b_idx;
+};
+hipError_t split_workspace_bytes(uint64_t n, size_t *bytes);
+hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes, bool nt, int max_blocks,
+                              hipStream_t stream);
 hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream);
 hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool nt, int max_blocks, uint32_t *out,
                               hipStream_t stream);

@@ -290,6 +290,115 @@ hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hi
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Split ragged batches: bodies whose bytes plus 16-B end pad fit a 1 KiB
+// quarter ("small") go four to a row through the QB = 4 rows kernel, the rest
+// one body per row sequence (QB = 1).  Flags, their exclusive scan (rocPRIM)
+// and an order-preserving scatter build both lists and their counts on the
+// device (no host round trip); each rows kernel reads its count from the
+// device and writes CRC i to out[idx[i]].  Frames batches (bodies <= 1 KiB,
+// rpc.h:17) take this path: almost every body is small.
+// ---------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ bool small_body(const uint8_t *base, uint64_t off, uint32_t len) {
+  const uint32_t z = (uint32_t)(0u - (uint32_t)((uint64_t)(uintptr_t)base + off + len)) & 15u;
+  return len + z <= 1024u;
+}
+
+__global__ void __launch_bounds__(256) split_flag_kernel(const uint8_t *base, const uint64_t *offsets,
+                                                         const uint32_t *lengths, uint64_t n, uint32_t *flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i < n) flag[i] = small_body(base, offsets[i], lengths[i]) ? 1u : 0u;
+}
+
+// Item i goes to slot pos[i] of the small list or slot i - pos[i] of the big
+// one (stable: both lists keep batch order, so consecutive tasks stay
+// neighbours in memory).  Thread n - 1 publishes both counts.
+__global__ void __launch_bounds__(256) split_scatter_kernel(const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+                                                            const uint32_t *flag, const uint32_t *pos,
+                                                            SplitLists l) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t f = flag[i], p = pos[i];
+  const uint64_t off = offsets[i];
+  const uint32_t len = lengths[i];
+  if (f) {
+    l.s_off[p] = off;
+    l.s_len[p] = len;
+    l.s_idx[p] = (uint32_t)i;
+  } else {
+    const uint64_t q = i - p;
+    l.b_off[q] = off;
+    l.b_len[q] = len;
+    l.b_idx[q] = (uint32_t)i;
+  }
+  if (i == n - 1) {
+    l.counts[0] = p + f;
+    l.counts[1] = n - (p + f);
+  }
+}
+
+hipError_t split_scan(void *tmp, size_t &bytes, const uint32_t *flag, uint32_t *pos, uint64_t n, hipStream_t s) {
+  return rocprim::exclusive_scan(tmp, bytes, flag, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
+}
+} // namespace
+
+hipError_t split_workspace_bytes(uint64_t n, size_t *bytes) {
+  size_t scan = 0;
+  const hipError_t e = split_scan(nullptr, scan, nullptr, nullptr, n, nullptr);
+  if (e != hipSuccess) return e;
+  *bytes = 2 * align256(n * 4) + align256(16) + 2 * (align256(n * 8) + 2 * align256(n * 4)) + align256(scan);
+  return hipSuccess;
+}
+
+hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes, bool nt, int max_blocks,
+                              hipStream_t s) {
+  const uint64_t n = proto.n_items;
+  if (n == 0) return hipSuccess;
+  if (n >= 0xFFFFFFFFull || proto.offsets == nullptr || proto.lengths == nullptr) return hipErrorInvalidValue;
+  uint8_t *w = static_cast<uint8_t *>(ws);
+  auto take = [&](size_t bytes) {
+    uint8_t *r = w;
+    w += align256(bytes);
+    return r;
+  };
+  uint32_t *flag = reinterpret_cast<uint32_t *>(take(n * 4));
+  uint32_t *pos = reinterpret_cast<uint32_t *>(take(n * 4));
+  SplitLists l;
+  l.counts = reinterpret_cast<uint64_t *>(take(16));
+  l.s_off = reinterpret_cast<uint64_t *>(take(n * 8));
+  l.s_len = reinterpret_cast<uint32_t *>(take(n * 4));
+  l.s_idx = reinterpret_cast<uint32_t *>(take(n * 4));
+  l.b_off = reinterpret_cast<uint64_t *>(take(n * 8));
+  l.b_len = reinterpret_cast<uint32_t *>(take(n * 4));
+  l.b_idx = reinterpret_cast<uint32_t *>(take(n * 4));
+  const size_t used = (size_t)(w - static_cast<uint8_t *>(ws));
+  if (used > ws_bytes) return hipErrorInvalidValue;
+  size_t scan = ws_bytes - used;
+  const dim3 g((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(split_flag_kernel, g, dim3(256), 0, s, proto.base, proto.offsets, proto.lengths, n, flag);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = split_scan(w, scan, flag, pos, n, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(split_scatter_kernel, g, dim3(256), 0, s, proto.offsets, proto.lengths, n, flag, pos, l);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  ItemsArgs a = proto; // small bodies, four per row
+  a.offsets = l.s_off;
+  a.lengths = l.s_len;
+  a.n_dev = l.counts;
+  a.out_idx = l.s_idx;
+  e = launch_rows(a, 4, nt, max_blocks, s);
+  if (e != hipSuccess) return e;
+  a.offsets = l.b_off; // the rest, one body per row sequence
+  a.lengths = l.b_len;
+  a.n_dev = l.counts + 1;
+  a.out_idx = l.b_idx;
+  return launch_rows(a, 1, nt, max_blocks, s);
+}
+
 hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream) {
   if (nbytes == 0) return hipSuccess;
   if (nbytes % 8 != 0) return hipErrorInvalidValue;

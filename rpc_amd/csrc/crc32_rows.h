@@ -426,7 +426,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   const uint32_t vb = (nblk % 8u == 0u) ? (blockIdx.x % 8u) * (nblk / 8u) + blockIdx.x / 8u : blockIdx.x;
   const uint64_t gw = (uint64_t)vb * 16u + wave;
   const uint32_t mode = a.mode;
-  const uint64_t n = a.n_items;
+  const uint64_t n = a.n_dev ? ld_const(a.n_dev, 0) : a.n_items;
+  auto oidx = [&](uint64_t i) -> uint64_t { return a.out_idx ? (uint64_t)a.out_idx[i] : i; }; // output slot
   const uint64_t n_tasks = (QB == 4) ? (n + 3) / 4 : n;
   // Group dealing, G = 2^a.gshift: in each whole round of nwaves * G tasks,
   // wave gw takes the G consecutive tasks [gw * G, gw * G + G), so its results
@@ -537,7 +538,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t sink = 0;
     auto flush = [&]() {
       if constexpr ((ABL & kRowsAblNoStore) == 0) {
-        if (lane < ocount) a.out[task_of(j0 + lane)] = outv;
+        if (lane < ocount) a.out[oidx(task_of(j0 + lane))] = outv;
       } else {
         sink ^= outv;
       }
@@ -567,7 +568,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       if (old + 1u == cnt) { // this wave completed the round
         const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
         if constexpr ((ABL & kRowsAblNoStore) == 0) {
-          if (lane < cnt) a.out[base + lane] = v;
+          if (lane < cnt) a.out[oidx(base + lane)] = v;
         } else {
           sink ^= v;
         }
@@ -827,8 +828,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         const uint64_t ibase = 4 * base;
         const uint32_t nit = (n - ibase < kW) ? (uint32_t)(n - ibase) : kW;
         const uint32_t v0 = ring[lane], v1 = ring[64 + lane];
-        if (lane < nit) a.out[ibase + lane] = v0;
-        if (64 + lane < nit) a.out[ibase + 64 + lane] = v1;
+        if (lane < nit) a.out[oidx(ibase + lane)] = v0;
+        if (64 + lane < nit) a.out[oidx(ibase + 64 + lane)] = v1;
         if (lane == 0) {
           done[slot] = 0;
           __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -838,7 +839,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     auto flush = [&]() {
       const uint64_t item = 4 * task_of(j0 + lane / 4u) + (lane & 3u);
-      if (lane < ocount && item < n) a.out[item] = outv;
+      if (lane < ocount && item < n) a.out[oidx(item)] = outv;
       j0 += ocount / 4u;
       ocount = 0;
     };

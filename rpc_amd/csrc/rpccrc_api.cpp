@@ -55,7 +55,8 @@ const uint64_t g_large_chunk = [] {
   return (v >= 16 && v % 16 == 0 && v <= (1ull << 31)) ? (uint64_t)v : (uint64_t)16384;
 }();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
-constexpr uint64_t kPackedMinBodies = 64;         // fewer bodies: one wave per body (rows kernel)
+constexpr uint64_t kPackedMinBodies = 64;         // fewer frames: one wave per body (rows kernel)
+constexpr bool kAutoSplitFrames = true;           // AUTO frames batches: split (true) or packed (false)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
 // Chunks per packed slice, at least: a slice switch costs the wave two scalar
 // loads it waits on.  Tuning override: RPCCRC_PACKED_MIN_SLICE.
@@ -159,14 +160,36 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
 }
 
 // A ragged batch on the device.  AUTO: frames (bodies capped at MAX_BODY_LEN =
-// 1 KiB, rpc.h:17) take the packed kernel (crc32_packed.h: four bodies per
-// row; 1.6x the rows kernel on 1M x 1 KiB), other batches the
-// rows kernel (one wave per body; ahead on C2's 64 B - 64 KiB mix).
+// 1 KiB, rpc.h:17) take the split path (bodies <= 1 KiB four per row through
+// the QB = 4 rows kernel: 1M frames 334 us vs 481 packed, 565 rows, DESIGN.md
+// 4.2), other batches the rows kernel (one wave per body; ahead on C2's
+// 64 B - 64 KiB mix).
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
            uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies = false) {
   const bool fits = n < (1ull << 27); // the packed kernel's metadata window: 8-B offsets in a 1 GiB buffer range
-  const bool packed = fits && (g_ragged_path == RPCCRC_RAGGED_PACKED ||
-                               (g_ragged_path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies));
+  const bool auto_frames = g_ragged_path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies;
+  const bool packed = fits && (g_ragged_path == RPCCRC_RAGGED_PACKED || (auto_frames && !kAutoSplitFrames));
+  const bool split = !packed && n < 0xFFFFFFFFull &&
+                     (g_ragged_path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
+  if (split) {
+    size_t bytes = 0;
+    RPCCRC_TRY(split_workspace_bytes(n, &bytes));
+    void *ws = nullptr;
+    RPCCRC_TRY(hipMallocAsync(&ws, bytes, s));
+    ItemsArgs a;
+    a.base = base;
+    a.offsets = offsets;
+    a.lengths = lengths;
+    a.n_items = n;
+    a.mode = mode;
+    a.lds_image = c.img;
+    a.tq = c.tq;
+    a.out = out;
+    a.gshift = kRowsGroupShift;
+    const int r = map_hip(launch_split_batch(a, ws, bytes, g_nontemporal != 0, max_blocks_for(c), s));
+    (void)hipFreeAsync(ws, s);
+    return r;
+  }
   if (!packed) return items(c, base, offsets, lengths, n, 0, 0, mode, out, 1, s);
   const uint64_t ms = std::min<uint64_t>(kPackedMaxSlices, std::max<uint64_t>(8192, 4 * n));
   size_t bytes = 0;
@@ -646,7 +669,9 @@ int rpc_crc32_set_options(int nontemporal, int max_blocks) {
 }
 
 int rpc_crc32_set_ragged_path(int path) {
-  if (path != RPCCRC_RAGGED_AUTO && path != RPCCRC_RAGGED_ROWS && path != RPCCRC_RAGGED_PACKED) return RPCCRC_EINVAL;
+  if (path != RPCCRC_RAGGED_AUTO && path != RPCCRC_RAGGED_ROWS && path != RPCCRC_RAGGED_PACKED &&
+      path != RPCCRC_RAGGED_SPLIT)
+    return RPCCRC_EINVAL;
   g_ragged_path = path;
   return RPCCRC_OK;
 }

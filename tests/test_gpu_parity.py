@@ -108,7 +108,7 @@ def test_device_uniform(body_len, pad):
     assert np.array_equal(got, oracle.crc32_uniform(host, n, body_len, stride))
 
 
-@pytest.fixture(params=["rows", "packed"])
+@pytest.fixture(params=["rows", "packed", "split"])
 def ragged_path(request):
     """Both ragged-batch kernels: one wavefront per body, and 1 KiB chunks packed four per row."""
     rpc_amd.set_ragged_path(request.param)
@@ -217,6 +217,26 @@ def test_device_batch_rows_workgroup_dynamic():
     rpc_amd.set_ragged_path("rows")
     try:
         _ragged_check(host, offs, lens)
+    finally:
+        rpc_amd.set_ragged_path("auto")
+
+
+@pytest.mark.parametrize("misalign", [0, 7])
+def test_device_batch_split_workgroup_dynamic(misalign):
+    """The split path on a large ragged batch: small bodies (<= 1 KiB with their
+    end pad, incl. 1009..1024 B bodies that fit or not by alignment) four per
+    row through the QB = 4 kernel with dynamic dealing, the rest through QB = 1,
+    both writing through the index lists; unordered and empty bodies."""
+    rng = np.random.default_rng(72 + misalign)
+    n = 300007
+    lens = np.where(rng.random(n) < 0.5, rng.integers(0, 1025, n), rng.integers(1000, 9000, n)).astype(np.uint32)
+    lens[::97] = 0
+    offs = _packed_offsets(lens, misalign)
+    perm = rng.permutation(n)  # batch order differs from memory order
+    host = oracle.splitmix_bytes(int(lens.sum()) + 64, 16)
+    rpc_amd.set_ragged_path("split")
+    try:
+        _ragged_check(host, offs[perm].copy(), lens[perm].copy())
     finally:
         rpc_amd.set_ragged_path("auto")
 
@@ -429,13 +449,14 @@ def test_c2_ragged_loguniform_sample():
     want = oracle.crc32_batch(base.cpu().numpy(), offs, lens)  # every body
     bad = np.flatnonzero(got != want)
     assert bad.size == 0, f"{bad.size} mismatches, first body {int(bad[0])}"
-    # every body: the two ragged kernels agree
-    rpc_amd.set_ragged_path("packed")
-    try:
-        packed = u32(rpc_amd.device_batch(base, doffs, dlens))
-    finally:
-        rpc_amd.set_ragged_path("auto")
-    assert np.array_equal(got, packed)
+    # every body: the ragged kernels agree
+    for path in ("packed", "split"):
+        rpc_amd.set_ragged_path(path)
+        try:
+            other = u32(rpc_amd.device_batch(base, doffs, dlens))
+        finally:
+            rpc_amd.set_ragged_path("auto")
+        assert np.array_equal(got, other), path
 
 
 def test_c4_large_bodies():

@@ -177,13 +177,22 @@ def packed_modes(a):
     dev = torch.device("cuda", 0)
     res = []
     shapes = [("4096x1M", 1 << 20, 4096), ("1024x1M", 1 << 20, 1024), ("3000x1M", 1 << 20, 3000),
-              ("c2", None, None)]
+              ("frames1M", 1 << 20, None), ("c2", None, None)]
     if a.shapes:
         shapes = [x for x in shapes if x[0] in a.shapes.split(",")]
     for name, n, L in shapes:
         if name == "c2":
             w = Workload("c2", 0, dev)
             base, offs, lens, nbytes = w.base, w.offs, w.lens, w.total
+        elif L is None:  # wire frames: 12-B header + body of 1..1024 B (rpc.h:17), back to back
+            rng = np.random.default_rng(11)
+            ln = rng.integers(1, 1025, n).astype(np.uint32)
+            fo = np.concatenate([[0], np.cumsum(ln[:-1].astype(np.uint64) + 12)]).astype(np.uint64)
+            nbytes = int(ln.sum())
+            base = torch.empty((int(fo[-1]) + 12 + int(ln[-1]) + 64) // 8 * 8, dtype=torch.uint8, device=dev)
+            rpc_amd.fill_random(base, 7)
+            offs = torch.from_numpy((fo + 12).view(np.int64)).to(dev)
+            lens = torch.from_numpy(ln.view(np.int32)).to(dev)
         else:
             nbytes = n * L
             base = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
