@@ -30,11 +30,13 @@ struct ItemsArgs {
   const uint32_t *out_idx = nullptr;
 };
 
+constexpr uint32_t kShiftNibWords = 64u * 8u * 16u; // 32 KiB: the chunk combine's shift maps
+
 struct CombineArgs {
   const uint32_t *raw;          // per-chunk crc0 values
   const uint64_t *lengths;      // body lengths (bytes)
   const uint64_t *chunk_first;  // index into raw of each body's chunk 0
-  const uint32_t *x2n_bytes;    // x^(8*2^k) mod P, k = 0..63
+  const uint4 *shift_nib;       // NIB[k][i][j] = A_{2^k bytes}(j << 4i), k < 64, i < 8, j < 16
   uint64_t n_bodies;
   uint64_t chunk;               // chunk size in bytes (multiple of 16)
   uint32_t *out;                // zeroed before the launch: blocks XOR their partials in

@@ -31,26 +31,36 @@ namespace rpccrc {
 // k = 0..nch-1 (end-aligned chunks of `chunk` bytes, all crc0) are folded into
 // crc(body) = ~(A_L(F) ^ XOR_k A_{(nch-1-k)*chunk}(raw_k)).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t dev_xpow_bytes(uint64_t nbytes, const uint32_t *x2n_bytes) {
-  // x2n_bytes[k] = x^(8 * 2^k) mod P, k = 0..63.
-  uint32_t r = kX0;
-  for (int k = 0; nbytes; ++k, nbytes >>= 1)
-    if (nbytes & 1u) r = gf2_mulmod(r, x2n_bytes[k]);
+// A_n(v) for n = sum of 2^k bytes, applied map by map from the nibble tables
+// NIB[k][i][j] = A_{2^k}(j << 4i) (64 maps x 8 nibble positions x 16, in LDS):
+// 8 lookups per set bit of n, instead of a bit-serial gf2_mulmod for x^(8n)
+// and another for the product (~30 of those per thread for C4's shifts).
+__device__ __forceinline__ uint32_t nib_apply(const uint32_t *nib, uint32_t k, uint32_t v) {
+  const uint32_t *m = nib + k * 128u;
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) r ^= m[i * 16u + ((v >> (4u * i)) & 15u)];
   return r;
+}
+__device__ __forceinline__ uint32_t nib_shift(const uint32_t *nib, uint64_t nbytes, uint32_t v) {
+  while (nbytes) {
+    const uint32_t k = (uint32_t)__builtin_ctzll(nbytes);
+    v = nib_apply(nib, k, v);
+    nbytes &= nbytes - 1;
+  }
+  return v;
 }
 
 // `splits` 256-thread blocks per body; block s folds a contiguous run of the
-// body's chunks.  Advancing a partial through one chunk, v -> A_chunk(v), is
-// GF(2)-linear, so it is 4 byte-table lookups: T[j][x] = A_chunk(x << 8j),
-// built in LDS by the block.  Thread t folds its run with Horner and shifts
+// body's chunks.  Thread t folds its part of the run with Horner (advancing a
+// partial through one chunk is A_chunk, a few nibble-table maps) and shifts
 // the partial to the body end; the block XORs its threads' partials and
 // atomically XORs the sum into out[b] (zeroed beforehand; block 0 adds the
 // ~A_L(0xFFFFFFFF) term, so out[b] ends as ~(A_L(F) ^ XOR_k ...)).  Several
-// blocks per body keep the chip busy with small chunks (1M chunks of 4 KiB
-// for C4: 16 blocks folding 65536 partials each took tens of microseconds).
+// blocks per body keep the chip busy with small chunks.
 constexpr uint32_t kCombineThreads = 256;
 __global__ void __launch_bounds__(kCombineThreads) crc32_chunk_combine_kernel(CombineArgs a) {
-  __shared__ uint32_t tab[4][256];
+  __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
   __shared__ uint32_t part[kCombineThreads / 64];
   const uint64_t b = blockIdx.x / a.splits;
   const uint32_t s = blockIdx.x % a.splits;
@@ -61,24 +71,25 @@ __global__ void __launch_bounds__(kCombineThreads) crc32_chunk_combine_kernel(Co
   const uint64_t pb = (nch + a.splits - 1) / a.splits;
   const uint64_t c0 = s * pb, c1 = (c0 + pb < nch) ? c0 + pb : nch;
   if (c0 >= c1) return; // (block-uniform) no chunks here; empty bodies stay 0
-  const uint32_t xchunk = dev_xpow_bytes(a.chunk, a.x2n_bytes);
+  {
+    uint4 *dst = reinterpret_cast<uint4 *>(nib);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) tab[j][t] = gf2_mulmod(xchunk, t << (8 * j));
+    for (uint32_t k = 0; k < kShiftNibWords / 4 / kCombineThreads; ++k)
+      dst[k * kCombineThreads + t] = a.shift_nib[k * kCombineThreads + t];
+  }
   __syncthreads();
   const uint64_t per = (c1 - c0 + kCombineThreads - 1) / kCombineThreads;
   const uint64_t k0 = c0 + t * per;
   const uint64_t k1 = (k0 + per < c1) ? k0 + per : c1;
   uint32_t acc = 0;
-  for (uint64_t k = k0; k < k1; ++k)
-    acc = tab[0][acc & 255u] ^ tab[1][(acc >> 8) & 255u] ^ tab[2][(acc >> 16) & 255u] ^ tab[3][acc >> 24] ^
-          a.raw[first + k];
-  if (k1 > k0 && k1 < nch) acc = gf2_mulmod(dev_xpow_bytes((nch - k1) * a.chunk, a.x2n_bytes), acc);
+  for (uint64_t k = k0; k < k1; ++k) acc = nib_shift(nib, a.chunk, acc) ^ a.raw[first + k];
+  if (k1 > k0 && k1 < nch) acc = nib_shift(nib, (nch - k1) * a.chunk, acc);
   for (int m = 1; m < 64; m <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, m, 64);
   if ((t & 63u) == 0) part[t >> 6] = acc;
   __syncthreads();
   if (t == 0) {
     for (uint32_t w = 1; w < kCombineThreads / 64; ++w) acc ^= part[w];
-    if (s == 0) acc ^= ~gf2_mulmod(dev_xpow_bytes(L, a.x2n_bytes), 0xFFFFFFFFu);
+    if (s == 0) acc ^= ~nib_shift(nib, L, 0xFFFFFFFFu);
     atomicXor(a.out + b, acc);
   }
 }

@@ -33,7 +33,7 @@ struct DeviceCtx {
   int cus = 0;
   uint4 *img = nullptr;   // LDS table image (v2 layout, 160 KiB)
   uint32_t *tq = nullptr;
-  uint32_t *x2n = nullptr; // x^(8*2^k) mod P, k = 0..63
+  uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
   int status = RPCCRC_ENODEV;
   char name[128] = {0};
   char arch[64] = {0};
@@ -100,11 +100,12 @@ void init_device(int dev) {
     c.status = RPCCRC_ENODEV;
     return;
   }
-  std::vector<uint32_t> img(kLdsBytesV2 / 4), tq(kTqEntries), x2n(64);
+  std::vector<uint32_t> img(kLdsBytesV2 / 4), tq(kTqEntries), nib(kShiftNibWords);
   build_tq(tq.data());
-  uint32_t sq = kX0 >> 8; // x^8 (one zero byte)
-  for (int k = 0; k < 64; ++k) {
-    x2n[k] = sq;
+  uint32_t sq = kX0 >> 8; // x^8 (one zero byte); squared: x^(8 * 2^k)
+  for (uint32_t k = 0; k < 64; ++k) {
+    for (uint32_t i = 0; i < 8; ++i)
+      for (uint32_t j = 0; j < 16; ++j) nib[k * 128 + i * 16 + j] = gf2_mulmod(sq, j << (4 * i));
     sq = gf2_mulmod(sq, sq);
   }
   int prev = 0;
@@ -113,13 +114,13 @@ void init_device(int dev) {
   hipError_t e = hipSuccess;
   e = (e == hipSuccess) ? hipMalloc(&c.img, kLdsBytesV2) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
-  e = (e == hipSuccess) ? hipMalloc(&c.x2n, 64 * 4) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
   if (e == hipSuccess) {
     build_lds_image_v2(img.data());
     e = hipMemcpy(c.img, img.data(), kLdsBytesV2, hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(c.x2n, x2n.data(), 64 * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);
   (void)hipSetDevice(prev);
   c.status = map_hip(e);
 }
@@ -222,9 +223,19 @@ struct BodyDesc {
   uint64_t chunk_first;
 };
 
-__global__ void expand_chunks_kernel(const BodyDesc *bodies, uint64_t nb, uint64_t chunk, uint64_t total_chunks,
-                                     uint64_t *item_off, uint32_t *item_len, uint64_t *lens, uint64_t *firsts,
-                                     uint32_t *out) {
+// Bodies of one large-body call: up to kInlineBodies travel in the kernel
+// arguments (no H2D copy in the stream: the copy and the two launch
+// boundaries around it cost ~17 us per C4 call, profiles/r01n), more go
+// through a device copy of the table.
+constexpr uint64_t kInlineBodies = 32;
+struct InlineBodies {
+  BodyDesc b[kInlineBodies];
+};
+
+template <class Bodies>
+__device__ __forceinline__ void expand_chunks(const Bodies &bodies, uint64_t nb, uint64_t chunk, uint64_t total_chunks,
+                                              uint64_t *item_off, uint32_t *item_len, uint64_t *lens, uint64_t *firsts,
+                                              uint32_t *out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < nb) {
     lens[t] = bodies[t].len;
@@ -244,6 +255,18 @@ __global__ void expand_chunks_kernel(const BodyDesc *bodies, uint64_t nb, uint64
   const uint64_t start = end > chunk ? end - chunk : 0;
   item_off[t] = b.off + start;
   item_len[t] = (uint32_t)(end - start);
+}
+
+__global__ void expand_chunks_kernel(const BodyDesc *bodies, uint64_t nb, uint64_t chunk, uint64_t total_chunks,
+                                     uint64_t *item_off, uint32_t *item_len, uint64_t *lens, uint64_t *firsts,
+                                     uint32_t *out) {
+  expand_chunks(bodies, nb, chunk, total_chunks, item_off, item_len, lens, firsts, out);
+}
+
+__global__ void expand_chunks_inline_kernel(InlineBodies bodies, uint64_t nb, uint64_t chunk, uint64_t total_chunks,
+                                            uint64_t *item_off, uint32_t *item_len, uint64_t *lens, uint64_t *firsts,
+                                            uint32_t *out) {
+  expand_chunks(bodies.b, nb, chunk, total_chunks, item_off, item_len, lens, firsts, out);
 }
 
 struct PinnedStage {
@@ -279,9 +302,14 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   if (chunk == 0) chunk = g_large_chunk;
   if (chunk % 16 != 0 || chunk > (1ull << 31)) return RPCCRC_EINVAL;
   uint64_t total = 0, max_nch = 0;
-  int rc = t_large_stage.reserve(n * sizeof(BodyDesc));
-  if (rc) return rc;
-  BodyDesc *bd = static_cast<BodyDesc *>(t_large_stage.ptr);
+  const bool inl = n <= kInlineBodies;
+  InlineBodies ib;
+  BodyDesc *bd = ib.b;
+  if (!inl) {
+    const int rc = t_large_stage.reserve(n * sizeof(BodyDesc));
+    if (rc) return rc;
+    bd = static_cast<BodyDesc *>(t_large_stage.ptr);
+  }
   for (uint64_t i = 0; i < n; ++i) {
     bd[i].off = h_offsets[i];
     bd[i].len = h_lengths[i];
@@ -303,15 +331,23 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   uint64_t *d_ioff = d_firsts + n;
   uint32_t *d_ilen = reinterpret_cast<uint32_t *>(d_ioff + total);
   uint32_t *d_raw = d_ilen + total;
-  hipError_t e = hipMemcpyAsync(d_bodies, bd, n * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
-  t_large_stage.mark(s);
-  if (e != hipSuccess) {
-    (void)hipFreeAsync(ws, s);
-    return map_hip(e);
+  hipError_t e = hipSuccess;
+  if (!inl) {
+    e = hipMemcpyAsync(d_bodies, bd, n * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
+    t_large_stage.mark(s);
+    if (e != hipSuccess) {
+      (void)hipFreeAsync(ws, s);
+      return map_hip(e);
+    }
   }
   const uint64_t threads = std::max<uint64_t>(total, n);
-  hipLaunchKernelGGL(expand_chunks_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, d_bodies, n,
-                     chunk, total, d_ioff, d_ilen, d_lens, d_firsts, d_out);
+  const dim3 eg((unsigned)((threads + 255) / 256));
+  if (inl)
+    hipLaunchKernelGGL(expand_chunks_inline_kernel, eg, dim3(256), 0, s, ib, n, chunk, total, d_ioff, d_ilen, d_lens,
+                       d_firsts, d_out);
+  else
+    hipLaunchKernelGGL(expand_chunks_kernel, eg, dim3(256), 0, s, d_bodies, n, chunk, total, d_ioff, d_ilen, d_lens,
+                       d_firsts, d_out);
   e = hipGetLastError();
   int r = map_hip(e);
   if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
@@ -320,7 +356,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     ca.raw = d_raw;
     ca.lengths = d_lens;
     ca.chunk_first = d_firsts;
-    ca.x2n_bytes = c.x2n;
+    ca.shift_nib = c.shift_nib;
     ca.n_bodies = n;
     ca.chunk = chunk;
     ca.out = d_out;
