@@ -32,15 +32,30 @@ struct ItemsArgs {
 
 constexpr uint32_t kShiftNibWords = 64u * 8u * 16u; // 32 KiB: the chunk combine's shift maps
 
+// A large body of rpc_crc32_device_large: bytes [off, off + len) of the base
+// buffer, its end-aligned chunks at raw[chunk_first ...].
+struct LargeBody {
+  uint64_t off;
+  uint64_t len;
+  uint64_t chunk_first;
+};
+// Up to kInlineBodies bodies travel in the kernel arguments (no H2D copy).
+constexpr uint64_t kInlineBodies = 32;
+struct InlineBodies {
+  LargeBody b[kInlineBodies];
+};
+
 struct CombineArgs {
   const uint32_t *raw;          // per-chunk crc0 values
-  const uint64_t *lengths;      // body lengths (bytes)
-  const uint64_t *chunk_first;  // index into raw of each body's chunk 0
+  const uint64_t *lengths;      // body lengths (bytes); unused when inline
+  const uint64_t *chunk_first;  // index into raw of each body's chunk 0; unused when inline
   const uint4 *shift_nib;       // NIB[k][i][j] = A_{2^k bytes}(j << 4i), k < 64, i < 8, j < 16
   uint64_t n_bodies;
   uint64_t chunk;               // chunk size in bytes (multiple of 16)
-  uint32_t *out;                // zeroed before the launch: blocks XOR their partials in
+  uint32_t *out;                // splits > 1: zeroed before the launch, blocks XOR their partials in
   uint32_t splits = 1;          // blocks per body (each folds a contiguous run of chunks)
+  bool inline_bodies = false;   // body table from `bodies` below (n_bodies <= kInlineBodies)
+  InlineBodies bodies;
 };
 
 // QB = 1: rows of 4 KiB of one item (any length); QB = 4: four items per row,

@@ -51,46 +51,68 @@ __device__ __forceinline__ uint32_t nib_shift(const uint32_t *nib, uint64_t nbyt
   return v;
 }
 
-// `splits` 256-thread blocks per body; block s folds a contiguous run of the
-// body's chunks.  Thread t folds its part of the run with Horner (advancing a
-// partial through one chunk is A_chunk, a few nibble-table maps) and shifts
-// the partial to the body end; the block XORs its threads' partials and
-// atomically XORs the sum into out[b] (zeroed beforehand; block 0 adds the
-// ~A_L(0xFFFFFFFF) term, so out[b] ends as ~(A_L(F) ^ XOR_k ...)).  Several
-// blocks per body keep the chip busy with small chunks.
-constexpr uint32_t kCombineThreads = 256;
-__global__ void __launch_bounds__(kCombineThreads) crc32_chunk_combine_kernel(CombineArgs a) {
+// `splits` blocks per body; block s folds a contiguous run [c0, c1) of the
+// body's chunks.  Thread t takes chunks c0 + t, c0 + t + NT, ... (the raw
+// loads of a wave are coalesced): Horner with the step map A_{NT*chunk} (one
+// nibble map when NT and chunk are powers of two), then a shift of the
+// partial from its last chunk to the body end.  The block XORs its threads'
+// partials.  splits == 1 (the common case: up to 64Ki chunks per body, NT =
+// 1024) stores ~(A_L(F) ^ XOR) directly; splits > 1 atomically XORs into
+// the zeroed out[b] (block 0 adds the ~A_L(0xFFFFFFFF) term).
+template <uint32_t NT>
+__global__ void __launch_bounds__(NT) crc32_chunk_combine_kernel(CombineArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
-  __shared__ uint32_t part[kCombineThreads / 64];
+  __shared__ uint32_t part[NT / 64];
   const uint64_t b = blockIdx.x / a.splits;
   const uint32_t s = blockIdx.x % a.splits;
   const uint32_t t = threadIdx.x;
-  const uint64_t L = a.lengths[b];
-  const uint64_t first = a.chunk_first[b];
+  const uint64_t L = a.inline_bodies ? a.bodies.b[b].len : a.lengths[b];
+  const uint64_t first = a.inline_bodies ? a.bodies.b[b].chunk_first : a.chunk_first[b];
   const uint64_t nch = (L + a.chunk - 1) / a.chunk;
   const uint64_t pb = (nch + a.splits - 1) / a.splits;
   const uint64_t c0 = s * pb, c1 = (c0 + pb < nch) ? c0 + pb : nch;
-  if (c0 >= c1) return; // (block-uniform) no chunks here; empty bodies stay 0
+  if (c0 >= c1) { // (block-uniform) no chunks here
+    if (a.splits == 1 && t == 0) a.out[b] = 0u; // empty body
+    return;
+  }
+  const uint64_t step = (uint64_t)NT * a.chunk;
+  const uint32_t *raw = a.raw + first;
+  // The raw loads of a batch of 16 chunks are issued together, the first
+  // batch before the table copy, so the two memory round trips overlap.
+  constexpr uint32_t kB = 16;
+  uint32_t r[kB];
+  uint64_t k = c0 + t;
+  auto load_batch = [&]() {
+#pragma unroll
+    for (uint32_t i = 0; i < kB; ++i) r[i] = (k + i * NT < c1) ? raw[k + i * NT] : 0u;
+  };
+  load_batch();
   {
     uint4 *dst = reinterpret_cast<uint4 *>(nib);
 #pragma unroll
-    for (uint32_t k = 0; k < kShiftNibWords / 4 / kCombineThreads; ++k)
-      dst[k * kCombineThreads + t] = a.shift_nib[k * kCombineThreads + t];
+    for (uint32_t q = 0; q < kShiftNibWords / 4 / NT; ++q) dst[q * NT + t] = a.shift_nib[q * NT + t];
   }
   __syncthreads();
-  const uint64_t per = (c1 - c0 + kCombineThreads - 1) / kCombineThreads;
-  const uint64_t k0 = c0 + t * per;
-  const uint64_t k1 = (k0 + per < c1) ? k0 + per : c1;
   uint32_t acc = 0;
-  for (uint64_t k = k0; k < k1; ++k) acc = nib_shift(nib, a.chunk, acc) ^ a.raw[first + k];
-  if (k1 > k0 && k1 < nch) acc = nib_shift(nib, (nch - k1) * a.chunk, acc);
+  while (k < c1) {
+#pragma unroll
+    for (uint32_t i = 0; i < kB; ++i)
+      if (k + i * NT < c1) acc = nib_shift(nib, step, acc) ^ r[i];
+    k += (uint64_t)kB * NT;
+    if (k < c1) load_batch();
+  }
+  if (c0 + t < c1) { // shift from this thread's last chunk to the body end
+    const uint64_t kl = c0 + t + (c1 - 1 - (c0 + t)) / NT * NT;
+    acc = nib_shift(nib, (nch - 1 - kl) * a.chunk, acc);
+  }
   for (int m = 1; m < 64; m <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, m, 64);
   if ((t & 63u) == 0) part[t >> 6] = acc;
   __syncthreads();
   if (t == 0) {
-    for (uint32_t w = 1; w < kCombineThreads / 64; ++w) acc ^= part[w];
+    for (uint32_t w = 1; w < NT / 64; ++w) acc ^= part[w];
     if (s == 0) acc ^= ~nib_shift(nib, L, 0xFFFFFFFFu);
-    atomicXor(a.out + b, acc);
+    if (a.splits == 1) a.out[b] = acc;
+    else atomicXor(a.out + b, acc);
   }
 }
 
@@ -193,7 +215,11 @@ hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream) {
   if (a.n_bodies == 0) return hipSuccess;
   const uint64_t blocks = a.n_bodies * a.splits;
   if (a.splits == 0 || blocks >= (1ull << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(crc32_chunk_combine_kernel, dim3((unsigned)blocks), dim3(kCombineThreads), 0, stream, a);
+  if (a.inline_bodies && a.n_bodies > kInlineBodies) return hipErrorInvalidValue;
+  if (a.splits == 1)
+    hipLaunchKernelGGL(crc32_chunk_combine_kernel<1024>, dim3((unsigned)blocks), dim3(1024), 0, stream, a);
+  else
+    hipLaunchKernelGGL(crc32_chunk_combine_kernel<256>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -217,20 +217,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
 
 // ---- large bodies: chunk expansion + combine --------------------------------
 
-struct BodyDesc {
-  uint64_t off;
-  uint64_t len;
-  uint64_t chunk_first;
-};
-
-// Bodies of one large-body call: up to kInlineBodies travel in the kernel
-// arguments (no H2D copy in the stream: the copy and the two launch
-// boundaries around it cost ~17 us per C4 call, profiles/r01n), more go
-// through a device copy of the table.
-constexpr uint64_t kInlineBodies = 32;
-struct InlineBodies {
-  BodyDesc b[kInlineBodies];
-};
+using BodyDesc = LargeBody;
 
 template <class Bodies>
 __device__ __forceinline__ void expand_chunks(const Bodies &bodies, uint64_t nb, uint64_t chunk, uint64_t total_chunks,
@@ -297,12 +284,41 @@ struct PinnedStage {
 
 thread_local PinnedStage t_large_stage;
 
+// Large bodies: end-aligned chunks, CRC'd by the rows kernel in RAW mode, then
+// folded per body by the chunk combine.
+//  * Contiguous fast path: when the bodies lie back to back and every length
+//    is a multiple of the chunk, the chunks of all bodies are one uniform
+//    batch (base + off_0 + i * chunk): the rows kernel runs the north-star
+//    pattern and no chunk table is built.  With the default chunk (0) the
+//    largest of 16/8/4 KiB dividing every length is taken.
+//  * Otherwise expand_chunks writes each chunk's (offset, length) and the rows
+//    kernel runs ragged.
+// <= 32 bodies travel in the kernel arguments; bodies of <= 64Ki chunks get
+// one 1024-thread combine block each (plain store), longer ones several
+// blocks that XOR into the zeroed output.
 int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_offsets, const uint64_t *h_lengths,
                  uint64_t n, uint32_t *d_out, uint64_t chunk, hipStream_t s) {
-  if (chunk == 0) chunk = g_large_chunk;
   if (chunk % 16 != 0 || chunk > (1ull << 31)) return RPCCRC_EINVAL;
-  uint64_t total = 0, max_nch = 0;
+  if (n == 0) return RPCCRC_OK;
   const bool inl = n <= kInlineBodies;
+  bool contiguous = inl;
+  uint64_t lens_or = 0;
+  for (uint64_t i = 0; i < n && contiguous; ++i) {
+    lens_or |= h_lengths[i];
+    if (i + 1 < n && h_offsets[i + 1] != h_offsets[i] + h_lengths[i]) contiguous = false;
+  }
+  if (chunk == 0) {
+    chunk = g_large_chunk;
+    if (contiguous && lens_or % chunk != 0 && !getenv("RPCCRC_LARGE_CHUNK"))
+      for (uint64_t cand : {8192ull, 4096ull})
+        if (lens_or % cand == 0) {
+          chunk = cand;
+          break;
+        }
+  }
+  // power-of-two chunk: every length is a multiple of it iff their OR is
+  const bool pow2 = (chunk & (chunk - 1)) == 0;
+  uint64_t total = 0, max_nch = 0;
   InlineBodies ib;
   BodyDesc *bd = ib.b;
   if (!inl) {
@@ -310,6 +326,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     if (rc) return rc;
     bd = static_cast<BodyDesc *>(t_large_stage.ptr);
   }
+  bool multiple = true;
   for (uint64_t i = 0; i < n; ++i) {
     bd[i].off = h_offsets[i];
     bd[i].len = h_lengths[i];
@@ -317,40 +334,54 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     const uint64_t nch = (h_lengths[i] + chunk - 1) / chunk;
     total += nch;
     max_nch = std::max(max_nch, nch);
+    if (!pow2 && h_lengths[i] % chunk != 0) multiple = false;
   }
+  if (pow2) multiple = lens_or % chunk == 0;
   if (total == 0) { // all bodies empty
     RPCCRC_TRY(hipMemsetAsync(d_out, 0, n * 4, s));
     return RPCCRC_OK;
   }
-  const size_t ws_bytes = n * sizeof(BodyDesc) + n * 16 + total * (8 + 4 + 4) + 64;
+  uint64_t splits = 1; // combine blocks per body
+  if (max_nch > 65536) {
+    splits = (max_nch + 1023) / 1024;
+    splits = std::max<uint64_t>(1, std::min<uint64_t>(splits, (1ull << 20) / n));
+  }
+  const bool fast = contiguous && multiple && splits == 1;
+  const size_t ws_bytes = fast ? total * 4 + 64 : n * sizeof(BodyDesc) + n * 16 + total * (8 + 4 + 4) + 64;
   uint8_t *ws = nullptr;
   RPCCRC_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), ws_bytes, s));
-  BodyDesc *d_bodies = reinterpret_cast<BodyDesc *>(ws);
-  uint64_t *d_lens = reinterpret_cast<uint64_t *>(ws + n * sizeof(BodyDesc));
-  uint64_t *d_firsts = d_lens + n;
-  uint64_t *d_ioff = d_firsts + n;
-  uint32_t *d_ilen = reinterpret_cast<uint32_t *>(d_ioff + total);
-  uint32_t *d_raw = d_ilen + total;
-  hipError_t e = hipSuccess;
-  if (!inl) {
-    e = hipMemcpyAsync(d_bodies, bd, n * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
-    t_large_stage.mark(s);
-    if (e != hipSuccess) {
-      (void)hipFreeAsync(ws, s);
-      return map_hip(e);
+  int r = RPCCRC_OK;
+  uint32_t *d_raw = reinterpret_cast<uint32_t *>(ws);
+  uint64_t *d_lens = nullptr, *d_firsts = nullptr;
+  if (fast) {
+    r = items(c, d_base + h_offsets[0], nullptr, nullptr, total, chunk, (uint32_t)chunk, kModeRaw, d_raw, 1, s);
+  } else {
+    BodyDesc *d_bodies = reinterpret_cast<BodyDesc *>(ws);
+    d_lens = reinterpret_cast<uint64_t *>(ws + n * sizeof(BodyDesc));
+    d_firsts = d_lens + n;
+    uint64_t *d_ioff = d_firsts + n;
+    uint32_t *d_ilen = reinterpret_cast<uint32_t *>(d_ioff + total);
+    d_raw = d_ilen + total;
+    hipError_t e = hipSuccess;
+    if (!inl) {
+      e = hipMemcpyAsync(d_bodies, bd, n * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
+      t_large_stage.mark(s);
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(ws, s);
+        return map_hip(e);
+      }
     }
+    const uint64_t threads = std::max<uint64_t>(total, n);
+    const dim3 eg((unsigned)((threads + 255) / 256));
+    if (inl)
+      hipLaunchKernelGGL(expand_chunks_inline_kernel, eg, dim3(256), 0, s, ib, n, chunk, total, d_ioff, d_ilen, d_lens,
+                         d_firsts, d_out);
+    else
+      hipLaunchKernelGGL(expand_chunks_kernel, eg, dim3(256), 0, s, d_bodies, n, chunk, total, d_ioff, d_ilen, d_lens,
+                         d_firsts, d_out);
+    r = map_hip(hipGetLastError());
+    if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
   }
-  const uint64_t threads = std::max<uint64_t>(total, n);
-  const dim3 eg((unsigned)((threads + 255) / 256));
-  if (inl)
-    hipLaunchKernelGGL(expand_chunks_inline_kernel, eg, dim3(256), 0, s, ib, n, chunk, total, d_ioff, d_ilen, d_lens,
-                       d_firsts, d_out);
-  else
-    hipLaunchKernelGGL(expand_chunks_kernel, eg, dim3(256), 0, s, d_bodies, n, chunk, total, d_ioff, d_ilen, d_lens,
-                       d_firsts, d_out);
-  e = hipGetLastError();
-  int r = map_hip(e);
-  if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
   if (r == RPCCRC_OK) {
     CombineArgs ca;
     ca.raw = d_raw;
@@ -360,10 +391,9 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     ca.n_bodies = n;
     ca.chunk = chunk;
     ca.out = d_out;
-    // blocks per body: about 1024 chunks each, at most 2^20 blocks in all
-    uint64_t sp = (max_nch + 1023) / 1024;
-    sp = std::max<uint64_t>(1, std::min<uint64_t>(sp, (1ull << 20) / n));
-    ca.splits = (uint32_t)sp;
+    ca.splits = (uint32_t)splits;
+    ca.inline_bodies = inl;
+    if (inl) ca.bodies = ib;
     r = map_hip(launch_chunk_combine(ca, s));
   }
   (void)hipFreeAsync(ws, s);

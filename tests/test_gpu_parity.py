@@ -265,8 +265,10 @@ def test_device_json_c0(golden):
     assert got[:16].tolist() == golden["json_c0"]["crcs"]
 
 
-@pytest.mark.parametrize("chunk", [0, 1024, 65536, 4096 + 16])
+@pytest.mark.parametrize("chunk", [0, 256, 1024, 65536, 4096 + 16])
 def test_device_large(chunk):
+    """Bodies with gaps between them: the chunk-table (expand) path; chunk 256
+    gives the 33 MiB body > 64Ki chunks (several combine blocks per body)."""
     lens = [0, 1, 17, 4096, (5 << 20) + 3, (33 << 20) + 11]
     offs, pos = [], 5
     for L in lens:
@@ -276,6 +278,34 @@ def test_device_large(chunk):
     got = u32(rpc_amd.device_large(to_dev(host), offs, lens, chunk=chunk))
     want = [oracle.crc32(host[o:o + L]) for o, L in zip(offs, lens)]
     assert got.tolist() == want
+
+
+@pytest.mark.parametrize("chunk,lens", [
+    (0, [16384, 0, 3 * 16384, (5 << 20), 16384 * 7]),      # default chunk 16 KiB, one empty body
+    (0, [4096 * 3, 8192, (1 << 20) + 4096]),               # default picks 4 KiB (lengths not multiples of 8 KiB)
+    (0, [8192 * 5, (2 << 20) + 8192]),                     # default picks 8 KiB
+    (4096, [4096] * 32),                                   # 32 bodies: the inline-table limit
+    (1024 + 16, [1040 * 3, 1040 * 100, 0, 1040]),          # chunk not a power of two
+    (256, [(17 << 20)]),                                   # > 64Ki chunks: falls back to the chunk table
+])
+def test_device_large_contiguous(chunk, lens):
+    """Back-to-back bodies whose lengths are multiples of the chunk: the uniform
+    fast path (one uniform rows launch + combine, no chunk table), at an odd base."""
+    offs, pos = [], 5
+    for L in lens:
+        offs.append(pos)
+        pos += L
+    host = oracle.splitmix_bytes(pos + 16, 4321)
+    got = u32(rpc_amd.device_large(to_dev(host), offs, lens, chunk=chunk))
+    want = [oracle.crc32(host[o:o + L]) for o, L in zip(offs, lens)]
+    assert got.tolist() == want
+    # 33 bodies (one past the inline table) with the same layout rule
+    if len(lens) == 32:
+        lens2 = lens + [4096]
+        offs2 = [5 + 4096 * i for i in range(33)]
+        host2 = oracle.splitmix_bytes(5 + 4096 * 33 + 16, 99)
+        got2 = u32(rpc_amd.device_large(to_dev(host2), offs2, lens2, chunk=chunk))
+        assert got2.tolist() == [oracle.crc32(host2[o:o + L]) for o, L in zip(offs2, lens2)]
 
 
 def test_nontemporal_option_same_result():
