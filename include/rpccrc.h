@@ -84,10 +84,11 @@ RPCCRC_API int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint3
 
 /* Large bodies (any size): body i = d_base[h_offsets[i] .. + h_lengths[i]),
  * offsets/lengths in HOST memory.  Each body is split into chunk_bytes chunks
- * (multiple of 16; 0 = default: 16 KiB)
- * processed in parallel and merged with the GF(2) combine (zlib crc32_combine
- * semantics), several combine blocks per body.  Stream-ordered; the call
- * returns once the work is enqueued. */
+ * (multiple of 16; 0 = default: 16 KiB, or 8/4 KiB when that divides every
+ * length of back-to-back bodies) processed in parallel and merged with the
+ * GF(2) combine (zlib crc32_combine semantics).  Back-to-back bodies whose
+ * lengths are chunk multiples run as one uniform batch.  Stream-ordered; the
+ * call returns once the work is enqueued. */
 RPCCRC_API int rpc_crc32_device_large(const uint8_t *d_base, const uint64_t *h_offsets, const uint64_t *h_lengths,
                            uint64_t n, uint32_t *d_out, uint64_t chunk_bytes, void *stream);
 
