@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--ragged-path", default="auto", choices=["auto", "rows", "packed", "split"],
                    help="ragged-batch kernel (C2): auto = rows for device batches; packed = 1 KiB chunks four per row")
     p.add_argument("--chunk-kib", type=int, default=0, help="C4: chunk size (0 = library default)")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="N>1 barrier backend: nccl (= RCCL over xGMI, the product); gloo only to rehearse "
+                        "several ranks on one GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
@@ -260,13 +263,19 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # one process per GPU; ranks beyond the visible GPUs (a gloo rehearsal on
+    # a 1-GPU box) share them
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
     if args.nontemporal >= 0:
         rpc_amd.set_options(nontemporal=bool(args.nontemporal))
     rpc_amd.set_ragged_path(args.ragged_path)
@@ -333,7 +342,8 @@ def main():
                 "body_len": w.L if w.kind != "ragged" else "log-uniform 64..65536",
                 "ragged_path": args.ragged_path if w.kind == "ragged" else None,
                 "bytes_per_gpu": w.total,
-                "parallelism": f"dp{world} (payload-index shards, RCCL barrier only)",
+                "parallelism": f"dp{world} (payload-index shards, "
+                               + ("RCCL barrier only)" if args.dist_backend == "nccl" or world == 1 else "gloo rehearsal barrier)"),
             },
             "roofline": {
                 "bound": "hbm",

@@ -311,6 +311,7 @@ constexpr int kRowsAblNoImage = 256;    // no LDS image copy (timing only; with 
 // the LDS image, and at exit, stored by lane 0 at times[4*gw + 0..2] together
 // with the wave's task count; times = a.offsets (unused by uniform batches).
 constexpr int kRowsAblTimes = 512;
+constexpr int kRowsAblNtStore = 2048; // non-temporal CRC stores (DYN paths; exact)
 
 namespace rows {
 
@@ -428,6 +429,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   const uint32_t mode = a.mode;
   const uint64_t n = a.n_dev ? ld_const(a.n_dev, 0) : a.n_items;
   auto oidx = [&](uint64_t i) -> uint64_t { return a.out_idx ? (uint64_t)a.out_idx[i] : i; }; // output slot
+  auto store_out = [&](uint32_t *p, uint32_t v) {
+    if constexpr ((ABL & kRowsAblNtStore) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+  };
   const uint64_t n_tasks = (QB == 4) ? (n + 3) / 4 : n;
   // Group dealing, G = 2^a.gshift: in each whole round of nwaves * G tasks,
   // wave gw takes the G consecutive tasks [gw * G, gw * G + G), so its results
@@ -568,7 +573,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       if (old + 1u == cnt) { // this wave completed the round
         const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
         if constexpr ((ABL & kRowsAblNoStore) == 0) {
-          if (lane < cnt) a.out[oidx(base + lane)] = v;
+          if (lane < cnt) store_out(a.out + oidx(base + lane), v);
         } else {
           sink ^= v;
         }
@@ -828,8 +833,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         const uint64_t ibase = 4 * base;
         const uint32_t nit = (n - ibase < kW) ? (uint32_t)(n - ibase) : kW;
         const uint32_t v0 = ring[lane], v1 = ring[64 + lane];
-        if (lane < nit) a.out[oidx(ibase + lane)] = v0;
-        if (64 + lane < nit) a.out[oidx(ibase + 64 + lane)] = v1;
+        if (lane < nit) store_out(a.out + oidx(ibase + lane), v0);
+        if (64 + lane < nit) store_out(a.out + oidx(ibase + 64 + lane), v1);
         if (lane == 0) {
           done[slot] = 0;
           __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

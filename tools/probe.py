@@ -86,9 +86,10 @@ def ablate_variants(w, a):
               (1, 1, 1, 259, 1), (1, 1, 1, 275, 1)]
     combos += [(1, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(1, 1, 1, 3, 1, 5), (1, 1, 1, 19, 1, 5)]
     combos += [(1, 1, 1, 1024, 1), (1, 1, 1, 1027, 1), (1, 1, 1, 1043, 1)]  # DYN (+ memory only)
+    combos += [(1, 1, 1, 3072, 1), (1, 1, 1, 1040, 1)]  # DYN with NT stores / no stores
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
-                   (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)] + [(4, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(4, 1, 1, 1024, 1)]
+                   (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)] + [(4, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(4, 1, 1, 1024, 1), (4, 1, 1, 1027, 1), (4, 1, 1, 1043, 1), (4, 1, 1, 1028, 1), (4, 1, 1, 3072, 1), (4, 1, 1, 1040, 1)]
 
     def name(c):
         return "qb{}_pair{}_nt{}_abl{}_d{}".format(*c[:5]) + (f"_g{c[5]}" if len(c) > 5 and c[5] else "")
