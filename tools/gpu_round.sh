@@ -74,6 +74,13 @@ for s in $STEPS; do
                python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
                python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive ;;
+    pmc_cfgs)
+           for c in ${PMC_CFGS:-c1 c2 c4}; do
+             run pmc_fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$c" -o run --output-format csv -- \
+                 python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive || exit 1
+             run pmc_write_$c 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$c" -o run --output-format csv -- \
+                 python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive || exit 1
+           done ;;
     pmcprobe)
            V=qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl6_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2
            run pmcprobe1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
