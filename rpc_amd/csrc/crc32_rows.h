@@ -768,18 +768,54 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       uint32_t lz[4];
       uint32_t sl;
     };
+    // Uniform batches with stride % 4 == 0: quarter b of group g is item 4g+b
+    // at base + (4g+b) * stride, and its end pad z_b = -(base + b*stride +
+    // len) mod 16 is the same for every g (4 * stride is a multiple of 16).
+    // So lz[b], the seeds and `full` are computed once, and a group whose four
+    // items all exist costs one 64-bit multiply instead of four quarter()
+    // calls and four seed loads (C1: the QB = 4 rows were bound by the scalar
+    // unit, PMC ~2.7x the SALU of a QB = 1 row).
+    const bool affine = !RAGGED && (a.stride % 4u) == 0;
+    QuarterInfo aq[4];
+    QuadMeta aqm;
+    bool afull = true;
+    aqm.sl = 0;
+    if constexpr (!RAGGED) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        aq[b].len = a.len;
+        aq[b].p0 = a.base + (uint64_t)b * a.stride;
+        aq[b].z = (uint32_t)(0u - (uint32_t)(uintptr_t)(aq[b].p0 + a.len)) & 15u;
+        aq[b].vstart = (int64_t)a.len + aq[b].z - (int64_t)kQuarter;
+        afull = afull && aq[b].vstart == 0 && a.len != 0;
+        aqm.lz[b] = (a.len << 4) | aq[b].z;
+        const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, a.len + aq[b].z);
+        aqm.sl = (hi == (uint32_t)b) ? seed : aqm.sl;
+      }
+    }
     auto issue = [&](uint64_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) -> QuadMeta {
       QuarterInfo qi[4];
       QuadMeta qm;
       bool full = ok;
       qm.sl = 0;
+      if (affine && ok && 4 * g + 4 <= n) {
+        const uint64_t gofs = 4 * g * a.stride;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        qi[b] = quarter(g, b);
-        full = full && qi[b].vstart == 0 && qi[b].len != 0;
-        qm.lz[b] = (qi[b].len << 4) | qi[b].z;
-        const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, qi[b].len + qi[b].z);
-        qm.sl = (hi == (uint32_t)b) ? seed : qm.sl;
+        for (int b = 0; b < 4; ++b) {
+          qi[b] = aq[b];
+          qi[b].p0 = aq[b].p0 + gofs;
+        }
+        qm = aqm;
+        full = afull;
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          qi[b] = quarter(g, b);
+          full = full && qi[b].vstart == 0 && qi[b].len != 0;
+          qm.lz[b] = (qi[b].len << 4) | qi[b].z;
+          const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, qi[b].len + qi[b].z);
+          qm.sl = (hi == (uint32_t)b) ? seed : qm.sl;
+        }
       }
       if constexpr ((ABL & kRowsAblNoLoad) != 0) {
         synth(g, buf);

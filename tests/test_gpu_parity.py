@@ -197,7 +197,11 @@ def test_device_batch_all_empty(ragged_path):
 
 
 @pytest.mark.parametrize("n,body_len,stride", [(65536 + 12345, 1500, 1500), (262144 + 4321, 200, 203),
-                                                (65536 * 2 + 31, 4096, 4096)])
+                                                (65536 * 2 + 31, 4096, 4096),
+                                                # QB = 4 affine metadata (stride % 4 == 0): pads z_b
+                                                # alternate 0/8 across quarters; last group partial
+                                                (262144 + 77, 1000, 1000), (262144 + 5, 500, 508),
+                                                (262144 + 2, 1024, 1024)])
 def test_device_uniform_workgroup_dynamic(n, body_len, stride):
     """Batches large enough for the workgroup-dynamic dealing (>= 8 rounds of 32
     tasks per workgroup), with a partial last round and pads z != 0."""
