@@ -173,11 +173,25 @@ def cpu_baseline(w: Workload, target_s: float):
     if sm > 0:
         reps = max(1, min(5000, int(math.ceil(target_s / sm))))
     sm, _ = ref.batch_timed(host, offs, lens, threads=threads, reps=reps)
+    # Config C0, the reference's own CPU case: 1024 x 4 KiB
+    # JSON-RPC bodies, crc.c at 1 thread and at `threads`, ~1 s each; the GPU's
+    # CRCs of the same bodies are checked equal.
+    c0_buf, c0_offs, c0_lens = oracle.json_bodies(1024, 4096, 0x5EED0001)
+    c0_bytes = int(c0_lens.sum(dtype=np.uint64))
+    c0 = {"sample": "1024 x 4096 B JSON-RPC bodies (seed 0x5EED0001)"}
+    for tn in sorted({1, threads}):
+        t1, c0_crc = ref.batch_timed(c0_buf, c0_offs, c0_lens, threads=tn, reps=1)
+        r = max(1, min(20000, int(math.ceil(1.0 / max(t1, 1e-6)))))
+        tr, _ = ref.batch_timed(c0_buf, c0_offs, c0_lens, threads=tn, reps=r)
+        c0[f"GiBps_{tn}_threads"] = round(c0_bytes * r / tr / GiB, 3)
+    c0_dev = rpc_amd.device_uniform(torch.from_numpy(c0_buf).to(w.device), 1024, 4096)
+    c0["gpu_crcs_match_reference"] = bool(np.array_equal(c0_dev.cpu().numpy().view(np.uint32), c0_crc))
     return {
         "value": round(nbytes * reps / sm / GiB, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": kind,
+        "c0": c0,
         "sample": f"{sample}, {reps} passes on {threads} threads ({sm:.1f} s)",
         "single_thread_value": round(nbytes / s1 / GiB, 3),
         "cpu_model": cpu_model(),
