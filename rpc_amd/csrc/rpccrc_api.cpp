@@ -284,6 +284,41 @@ struct PinnedStage {
 
 thread_local PinnedStage t_large_stage;
 
+// Per-thread device workspace, reused by the next call on the same stream
+// (stream order makes the reuse safe) and grown when too small.  A
+// hipFreeAsync per call blocked the calling thread until the GPU reached it
+// and left a ~6 us gap in the stream before the next call's first kernel
+// (rocprofv3 --hip-runtime-trace, profiles/r01h_*).  Released (stream-ordered)
+// when the thread switches stream or device; a thread's last workspace is
+// kept until the process ends.
+struct StreamWorkspace {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  void *p = nullptr;
+  size_t cap = 0;
+  int get(int device, hipStream_t s, size_t bytes, void **out) {
+    if (p && (dev != device || stream != s || cap < bytes)) {
+      int cur = -1;
+      (void)hipGetDevice(&cur);
+      if (cur != dev) (void)hipSetDevice(dev);
+      (void)hipFreeAsync(p, stream);
+      if (cur != dev) (void)hipSetDevice(cur);
+      p = nullptr;
+      cap = 0;
+    }
+    if (!p) {
+      const size_t want = std::max<size_t>(bytes, 1u << 20);
+      RPCCRC_TRY(hipMallocAsync(&p, want, s));
+      cap = want;
+      dev = device;
+      stream = s;
+    }
+    *out = p;
+    return RPCCRC_OK;
+  }
+};
+thread_local StreamWorkspace t_large_ws;
+
 // Large bodies: end-aligned chunks, CRC'd by the rows kernel in RAW mode, then
 // folded per body by the chunk combine.
 //  * Contiguous fast path: when the bodies lie back to back and every length
@@ -349,7 +384,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   const bool fast = contiguous && multiple && splits == 1;
   const size_t ws_bytes = fast ? total * 4 + 64 : n * sizeof(BodyDesc) + n * 16 + total * (8 + 4 + 4) + 64;
   uint8_t *ws = nullptr;
-  RPCCRC_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), ws_bytes, s));
+  if (const int rc = t_large_ws.get(c.device, s, ws_bytes, reinterpret_cast<void **>(&ws))) return rc;
   int r = RPCCRC_OK;
   uint32_t *d_raw = reinterpret_cast<uint32_t *>(ws);
   uint64_t *d_lens = nullptr, *d_firsts = nullptr;
@@ -367,7 +402,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
       e = hipMemcpyAsync(d_bodies, bd, n * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
       t_large_stage.mark(s);
       if (e != hipSuccess) {
-        (void)hipFreeAsync(ws, s);
+        // the workspace stays cached for the next call on this stream
         return map_hip(e);
       }
     }
@@ -396,7 +431,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     if (inl) ca.bodies = ib;
     r = map_hip(launch_chunk_combine(ca, s));
   }
-  (void)hipFreeAsync(ws, s);
+  // the workspace stays cached for the next call on this stream (no hipFreeAsync)
   return r;
 }
 
