@@ -288,9 +288,9 @@ thread_local PinnedStage t_large_stage;
 // (stream order makes the reuse safe) and grown when too small.  A
 // hipFreeAsync per call blocked the calling thread until the GPU reached it
 // and left a ~6 us gap in the stream before the next call's first kernel
-// (rocprofv3 --hip-runtime-trace, profiles/r01h_*).  Released (stream-ordered)
-// when the thread switches stream or device; a thread's last workspace is
-// kept until the process ends.
+// (rocprofv3 --hip-runtime-trace, profiles/r01h_*).  Released when the thread
+// switches stream or device or needs more; a thread's last workspace is kept
+// until the process ends.
 struct StreamWorkspace {
   int dev = -1;
   hipStream_t stream = nullptr;
@@ -298,10 +298,13 @@ struct StreamWorkspace {
   size_t cap = 0;
   int get(int device, hipStream_t s, size_t bytes, void **out) {
     if (p && (dev != device || stream != s || cap < bytes)) {
+      // hipFree, not hipFreeAsync on the old stream: the caller may have
+      // destroyed that stream by now.  hipFree waits for the device, so no
+      // queued work still uses the old workspace (only on a switch or growth).
       int cur = -1;
       (void)hipGetDevice(&cur);
       if (cur != dev) (void)hipSetDevice(dev);
-      (void)hipFreeAsync(p, stream);
+      (void)hipFree(p);
       if (cur != dev) (void)hipSetDevice(cur);
       p = nullptr;
       cap = 0;
