@@ -7,9 +7,11 @@ Metric (BASELINE.json): "GiB/s CRC32 over device-resident batched bodies;
 1M x 4 KiB bodies per GPU (weak scaling), synthetic splitmix64 bytes generated
 on the device.  Other BASELINE configs: --config c1 | c2 | c3 | c4.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under
-torch.distributed.run; one process per GPU, RCCL used only as the barrier).
-Rank 0 prints ONE JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W].  N>1: one process per
+GPU under torch.distributed.run -- either the driver's own launch, or, when
+WORLD_SIZE is not set, bench.py starts that launcher as a CHILD process itself
+(before importing torch or touching a GPU) and exits with its code.  RCCL is
+used only as the barrier.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -22,13 +24,14 @@ import sys
 import time
 
 import numpy as np
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-import rpc_amd  # noqa: E402
-from rpc_amd.shard import barrier, max_over_ranks, rank_seed, shard_range, sum_over_ranks  # noqa: E402
+# torch and rpc_amd (which loads the HIP runtime) are imported by main() only
+# after the N>1 self-launch decision: the launching parent never touches a GPU.
+torch = None
+rpc_amd = None
 
 METRIC = "GiB/s CRC32 over device-resident batched bodies; 1/2/4/8 MI355X"
 HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -62,6 +65,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
+    p.add_argument("--master-port", type=int, default=0, help="N>1 self-launch: rendezvous port (0 = pick a free one)")
+    p.add_argument("--no-scalar-latency", action="store_true")
     p.add_argument("--prewarm-s", type=float, default=0.5,
                    help="untimed steps before the W warmup steps until this much time has passed: the GPU "
                         "clock ramps over the first ~20 launches of sustained load (DESIGN.md 5)")
@@ -73,6 +78,8 @@ class Workload:
         desc, kind, n, L, seed = CONFIGS[cfg]
         self.name, self.desc, self.kind, self.n, self.L = cfg, desc, kind, n, L
         self.chunk = chunk
+        from rpc_amd.shard import rank_seed
+
         self.seed = rank_seed(seed, rank)
         self.device = device
         if kind == "uniform":
@@ -132,6 +139,15 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup allows (cpu.max quota / period), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(w: Workload, target_s: float):
     """The reference crc.c (+ system libz, built into oracle/_ref) timed on this
     host's cores over a bounded sample of the same workload."""
@@ -142,7 +158,7 @@ def cpu_baseline(w: Workload, target_s: float):
     kind = "reference"
     if ref is None:
         return None
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = max(1, len(os.sched_getaffinity(0)))  # every CPU this process may run on
     if w.kind == "uniform":
         nb = min(w.n, (256 << 20) // w.L)
         host = w.base[: nb * w.L].cpu().numpy()
@@ -190,6 +206,7 @@ def cpu_baseline(w: Workload, target_s: float):
         "value": round(nbytes * reps / sm / GiB, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "cgroup_cpu_quota": cgroup_cpu_quota(),
         "kind": kind,
         "c0": c0,
         "sample": f"{sample}, {reps} passes on {threads} threads ({sm:.1f} s)",
@@ -239,6 +256,24 @@ def rx_ring_probe():
     return r
 
 
+def scalar_latency_probe():
+    """Per-call latency of the drop-in rpc_crc32 (one GPU kernel per call) at 12 B,
+    68 B and 1 KiB on 1 and 10 threads, beside the reference crc.c on the same host
+    (tools/scalar_bench.c; VERDICT r01 'scalar path: measure it')."""
+    import subprocess
+    exe = os.path.join(REPO, "tools", "scalar_bench")
+    if not os.path.exists(exe):
+        return None
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_crc.so")
+    p = subprocess.run([exe] + ([ref] if os.path.exists(ref) else []), capture_output=True, text=True, timeout=300)
+    try:
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": (p.stderr or p.stdout)[-300:], "rc": p.returncode}
+    r["rc"] = p.returncode
+    return r
+
+
 def stream_read_probe(w: Workload, reps=10):
     """Achievable HBM read rate on the same buffer: a pure streaming read with
     coalesced 16-B lanes, non-temporal (the CRC kernel's load shape) and
@@ -269,14 +304,49 @@ def load_traffic(cfg: str):
         return None
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: start torch.distributed.run (one process per
+    GPU, 127.0.0.1 rendezvous) as a child with the same arguments and return its exit
+    code.  Runs before torch is imported here, so this parent never touches a GPU."""
+    import subprocess
+
+    port = args.master_port or free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
+    if os.environ.get("RPCCRC_BENCH_LAUNCH_ONLY"):  # CPU rehearsal of the launch path (tests/test_bench_launch.py)
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus,
+                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+        return
+    global torch, rpc_amd
+    import torch as _torch
+
+    import rpc_amd as _rpc_amd
+
+    torch, rpc_amd = _torch, _rpc_amd
+    from rpc_amd.shard import barrier, max_over_ranks, sum_over_ranks
+
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
     # one process per GPU; ranks beyond the visible GPUs (a gloo rehearsal on
     # a 1-GPU box) share them
     dev_index = local_rank % max(1, torch.cuda.device_count())
@@ -308,18 +378,22 @@ def main():
     if dist:
         barrier(dist, device)
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # One event per step boundary on the kernel's stream: per-launch durations
+    # (mean = roofline.achieved, median reported beside it).
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    evs[0].record(stream)
+    for k in range(args.steps):
         w.step()
-    ev1.record(stream)
+        evs[k + 1].record(stream)
     torch.cuda.synchronize()
     if dist:
         barrier(dist, device)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # avg launch duration on the kernel's stream
+    step_s = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(args.steps)]
+    kernel_s = sum(step_s) / args.steps  # avg launch duration on the kernel's stream
+    median_s = float(np.median(step_s))
     tmax = max_over_ranks(dist, wall, device) if dist else wall
     total_bytes = sum_over_ranks(dist, w.total, device) if dist else w.total
 
@@ -331,6 +405,8 @@ def main():
             extra["host_inclusive"] = host_inclusive(w)
             if w.kind == "uniform":
                 extra["rx_ring"] = rx_ring_probe()
+        if not args.no_scalar_latency and not args.no_host_inclusive:
+            extra["scalar_latency"] = scalar_latency_probe()
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(w, args.cpu_seconds)
 
@@ -371,6 +447,7 @@ def main():
                            else "crc32_rows_kernel",
                            "large": "crc32_rows_kernel (+chunk combine)"}[w.kind],
                 "avg_launch_us": round(kernel_s * 1e6, 2),
+                "median_launch_us": round(median_s * 1e6, 2),
                 "algo_bytes_per_launch": w.algo_bytes,
             },
             "cpu_baseline": cpu,

@@ -74,7 +74,9 @@ RPCCRC_API int64_t rpc_crc32_verify_batch(const uint8_t *base, const uint64_t *o
 /* ---- batched, device (HBM-resident) buffers ---------------------------- */
 
 /* Ragged batch: body i = d_base[d_offsets[i] .. + d_lengths[i]).  All pointers
- * are device pointers on the current device.  Asynchronous on `stream`. */
+ * are device pointers on the current device.  Asynchronous on `stream`.
+ * Bodies of >= 256 KiB are cut into chunks on the device and folded with the
+ * GF(2) combine, so one long body does not serialise the batch on one wave. */
 RPCCRC_API int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
                            uint64_t n, uint32_t *d_out, void *stream);
 
@@ -94,20 +96,55 @@ RPCCRC_API int rpc_crc32_device_large(const uint8_t *d_base, const uint64_t *h_o
 
 /* ---- frames (rpc.h:3-8 wire format) ------------------------------------ */
 
-/* Verify a contiguous device stream of n frames, each a 12-byte big-endian
- * rpc_header_t {u16 version, u16 type, u32 body_len, u32 crc32} followed by
- * body_len body bytes (reference rpc.h:3-15; parse as rpc_server_main.c:165-169).
- * d_frame_offsets[i] = byte offset of frame i's header.  d_ok[i] = 1 when the
- * body CRC equals the header CRC (PING/PONG frames with body_len 0 and crc 0
- * verify as 1, as rpc_server_main.c:172-187 short-circuits them). */
-RPCCRC_API int rpc_frames_verify_device(const uint8_t *d_stream, const uint64_t *d_frame_offsets, uint64_t n,
-                             uint8_t *d_ok, uint32_t *d_crc, void *stream);
+/* Reference wire constants (rpc.h:11-18). */
+#define RPC_HEADER_LEN_BYTES 12u /* RPC_HEADER_LEN, rpc.h:15 */
+#define RPC_MAX_BODY_LEN 1024u   /* MAX_BODY_LEN, rpc.h:17 */
+#define RPC_FRAME_TYPE_DATA 0u   /* RPC_TYPE_DATA, rpc.h:11 */
+#define RPC_FRAME_TYPE_PING 1u   /* RPC_TYPE_PING, rpc.h:12 */
+#define RPC_FRAME_TYPE_PONG 2u   /* RPC_TYPE_PONG, rpc.h:13 */
 
-/* Stamp headers: for each frame i write its 12-byte header (version, type,
- * body_len, crc32 big-endian, as rpc_async.c:521-530) at d_stream +
- * d_frame_offsets[i]; the body must already follow the header. */
-RPCCRC_API int rpc_frames_stamp_device(uint8_t *d_stream, const uint64_t *d_frame_offsets, const uint32_t *d_body_lens,
-                            uint64_t n, uint16_t version, uint16_t type, void *stream);
+/* Per-frame verdict (one byte per frame), in the order the reference decides:
+ * type first, then the body-length cap, then the CRC. */
+#define RPC_FRAME_BAD_CRC 0u   /* data frame, body CRC != header crc32: the server
+                                  closes the connection (rpc_server_main.c:227-233),
+                                  the client reports RPC_CRC_ERR (rpc_async.c:219-222) */
+#define RPC_FRAME_OK 1u        /* data frame, body CRC == header crc32 */
+#define RPC_FRAME_CONTROL 2u   /* heartbeat answered from the header alone, whatever
+                                  its crc32 / body_len fields hold: PING at the server
+                                  (rpc_server_main.c:172-187), PONG at the client
+                                  (rpc_async.c:303-309); no body is read */
+#define RPC_FRAME_TOO_LARGE 3u /* body_len > MAX_BODY_LEN with the cap in force: the
+                                  peer is dropped before its body is read
+                                  (rpc_server_main.c:189-195, rpc_async.c:312) */
+#define RPC_FRAME_MALFORMED 4u /* header or body extends past the stream: not read */
+
+/* Frame-call flags.  The role picks which heartbeat type is a control frame
+ * (the other one is an ordinary data frame, as in the reference). */
+#define RPC_FRAMES_SERVER 0x1   /* PING is control (rpc_server_main.c:172) */
+#define RPC_FRAMES_CLIENT 0x2   /* PONG is control (rpc_async.c:303) */
+#define RPC_FRAMES_LIFT_CAP 0x4 /* no MAX_BODY_LEN cap; bodies of any
+                                   size, the large ones chunked + GF(2)-combined */
+
+/* Verify n frames of a device stream of stream_bytes bytes.  Frame i starts at
+ * d_stream + d_frame_offsets[i] with a 12-byte big-endian rpc_header_t {u16
+ * version, u16 type, u32 body_len, u32 crc32} (rpc.h:3-8, parsed as
+ * rpc_server_main.c:165-169) followed by body_len body bytes.  Writes
+ * d_verdict[i] (RPC_FRAME_*) and, if d_crc is not NULL, the body CRC (0 for
+ * frames whose body is not read).  Nothing outside [d_stream, d_stream +
+ * stream_bytes) is read.  flags: exactly one role bit, optionally LIFT_CAP. */
+RPCCRC_API int rpc_frames_verify_device(const uint8_t *d_stream, uint64_t stream_bytes, const uint64_t *d_frame_offsets,
+                             uint64_t n, int flags, uint8_t *d_verdict, uint32_t *d_crc, void *stream);
+
+/* Stamp headers: for each frame i whose body d_stream[d_frame_offsets[i] + 12
+ * .. + d_body_lens[i]) lies inside the stream, write its 12-byte header
+ * (version, type, body_len, crc32 big-endian, as rpc_async.c:521-530).
+ * Without RPC_FRAMES_LIFT_CAP a body over MAX_BODY_LEN is not stamped (the
+ * reference client refuses to send it, rpc_async.c:499-501).  d_verdict
+ * (optional): RPC_FRAME_OK (stamped), _TOO_LARGE or _MALFORMED.  Role bits are
+ * ignored. */
+RPCCRC_API int rpc_frames_stamp_device(uint8_t *d_stream, uint64_t stream_bytes, const uint64_t *d_frame_offsets,
+                            const uint32_t *d_body_lens, uint64_t n, uint16_t version, uint16_t type, int flags,
+                            uint8_t *d_verdict, void *stream);
 
 /* ---- batched server receive ring -------------------
  * Replaces the one-frame-at-a-time verify of the reference server loop
@@ -129,19 +166,25 @@ typedef struct {
   uint16_t version;
   uint16_t type;
   uint32_t header_crc;  /* the crc32 the sender stamped */
-  uint32_t crc;         /* rpc_crc32 of the body, computed on the GPU */
-  uint8_t ok;           /* crc == header_crc: rpc_crc32_verify (PING/PONG: 1) */
+  uint32_t crc;         /* rpc_crc32 of the body, computed on the GPU (0 if not read) */
+  uint8_t ok;           /* verdict is RPC_FRAME_OK or RPC_FRAME_CONTROL */
+  uint8_t verdict;      /* RPC_FRAME_* */
 } rpc_rx_frame_t;
 
-/* nsegments (2..64) segments of segment_bytes bytes and max_frames frames each. */
-RPCCRC_API int rpc_rx_ring_create(rpc_rx_ring_t **ring, size_t segment_bytes, size_t max_frames, int nsegments);
+/* nsegments (2..64) segments of segment_bytes bytes and max_frames frames each;
+ * flags as rpc_frames_verify_device (one role bit, optionally LIFT_CAP). */
+RPCCRC_API int rpc_rx_ring_create(rpc_rx_ring_t **ring, size_t segment_bytes, size_t max_frames, int nsegments,
+                                  int flags);
 RPCCRC_API void rpc_rx_ring_destroy(rpc_rx_ring_t *ring);
 /* *dst = where to land a frame of frame_len bytes (header + body).  A segment
  * that cannot take it is submitted first; RPCCRC_EAGAIN when every segment is
  * still in flight or unpolled (call rpc_rx_ring_poll). */
 RPCCRC_API int rpc_rx_ring_reserve(rpc_rx_ring_t *ring, size_t frame_len, uint8_t **dst);
-/* Accepts the reserved frame; RPCCRC_EINVAL (frame dropped) unless its header
- * body_len + 12 equals the reserved length. */
+/* Accepts the reserved frame; RPCCRC_EINVAL (frame dropped) unless the landed
+ * length is what the reference reads for that header: 12 + body_len for a data
+ * frame, or the 12-byte header alone for a control frame or a data frame over
+ * the cap (the reference reads no body for either, rpc_server_main.c:172-195,
+ * rpc_async.c:303-315). */
 RPCCRC_API int rpc_rx_ring_commit(rpc_rx_ring_t *ring, uint64_t tag);
 /* reserve + memcpy + commit. */
 RPCCRC_API int rpc_rx_ring_push(rpc_rx_ring_t *ring, const void *frame, size_t frame_len, uint64_t tag);

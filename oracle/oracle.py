@@ -94,6 +94,78 @@ def crc32_uniform(buf: np.ndarray, n: int, body_len: int, stride: int | None = N
     return out
 
 
+# ---- frame verdicts (the reference's receive-side decisions) -------------------
+
+FRAME_BAD_CRC, FRAME_OK, FRAME_CONTROL, FRAME_TOO_LARGE, FRAME_MALFORMED = 0, 1, 2, 3, 4
+MAX_BODY_LEN = 1024  # rpc.h:17
+RPC_TYPE_PING, RPC_TYPE_PONG = 1, 2  # rpc.h:12-13
+
+
+def frame_verdict(stream: bytes, off: int, role: str = "server", lift_cap: bool = False) -> tuple[int, int]:
+    """(verdict, body crc) of the frame at ``off``, restating the reference's order:
+    parse the 12-byte big-endian header (rpc_server_main.c:165-169 / rpc_async.c:296-300);
+    a server answers PING from the header alone (rpc_server_main.c:172-187), a client
+    consumes PONG the same way (rpc_async.c:303-309); a body_len over MAX_BODY_LEN drops
+    the peer before the body is read (rpc_server_main.c:189-195, rpc_async.c:312-315);
+    otherwise the body is read and rpc_crc32_verify decides (rpc_server_main.c:227,
+    rpc_async.c:219).  MALFORMED: the frame does not fit the stream (our bound)."""
+    if off + 12 > len(stream):
+        return FRAME_MALFORMED, 0
+    h = stream[off:off + 12]
+    typ = int.from_bytes(h[2:4], "big")
+    blen = int.from_bytes(h[4:8], "big")
+    hcrc = int.from_bytes(h[8:12], "big")
+    if (role == "server" and typ == RPC_TYPE_PING) or (role == "client" and typ == RPC_TYPE_PONG):
+        return FRAME_CONTROL, 0
+    if blen > MAX_BODY_LEN and not lift_cap:
+        return FRAME_TOO_LARGE, 0
+    if off + 12 + blen > len(stream):
+        return FRAME_MALFORMED, 0
+    c = crc32(np.frombuffer(stream, dtype=np.uint8)[off + 12:off + 12 + blen]) if blen else 0
+    return (FRAME_OK if c == hcrc else FRAME_BAD_CRC), c
+
+
+def crc32_uniform_mt(buf: np.ndarray, n: int, body_len: int, threads: int = 16) -> np.ndarray:
+    """crc32_uniform over `threads` threads (the C oracle releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    out = np.empty(n, dtype=np.uint32)
+    b = np.ascontiguousarray(buf)
+    step = (n + threads - 1) // threads
+
+    def part(k):
+        lo, hi = k * step, min(n, (k + 1) * step)
+        if lo < hi:
+            _o.oracle_crc32_uniform(b.ctypes.data + lo * body_len, hi - lo, body_len, body_len,
+                                    out.ctypes.data + lo * 4)
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(part, range(threads)))
+    return out
+
+
+def crc32_batch_mt(buf: np.ndarray, offsets, lengths, threads: int = 16) -> np.ndarray:
+    """crc32_batch over `threads` threads."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = off.shape[0]
+    out = np.empty(n, dtype=np.uint32)
+    b = np.ascontiguousarray(buf)
+    step = (n + threads - 1) // threads
+
+    def part(k):
+        lo, hi = k * step, min(n, (k + 1) * step)
+        if lo < hi:
+            _o.oracle_crc32_batch(b.ctypes.data, off.ctypes.data + lo * 8, ln.ctypes.data + lo * 4, hi - lo,
+                                  out.ctypes.data + lo * 4)
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(part, range(threads)))
+    return out
+
+
 # ---- synthetic inputs (shared with bench.py and the device datagen kernel) ----
 
 GOLDEN = 0x9E3779B97F4A7C15

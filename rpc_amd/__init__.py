@@ -45,13 +45,30 @@ __all__ = [
     "RPC_TYPE_DATA",
     "RPC_TYPE_PING",
     "RPC_TYPE_PONG",
+    "MAX_BODY_LEN",
+    "FRAME_BAD_CRC",
+    "FRAME_OK",
+    "FRAME_CONTROL",
+    "FRAME_TOO_LARGE",
+    "FRAME_MALFORMED",
 ]
 
-# reference rpc.h:11-15
+# reference rpc.h:11-17
 RPC_TYPE_DATA = 0
 RPC_TYPE_PING = 1
 RPC_TYPE_PONG = 2
 RPC_HEADER_LEN = 12
+MAX_BODY_LEN = 1024
+
+# frame verdicts and flags (include/rpccrc.h RPC_FRAME_* / RPC_FRAMES_*)
+FRAME_BAD_CRC = 0
+FRAME_OK = 1
+FRAME_CONTROL = 2
+FRAME_TOO_LARGE = 3
+FRAME_MALFORMED = 4
+FRAMES_SERVER = 0x1
+FRAMES_CLIENT = 0x2
+FRAMES_LIFT_CAP = 0x4
 
 
 def _as_buffer(data) -> tuple[Optional[int], int, object]:
@@ -182,22 +199,46 @@ def device_large(base, offsets: Iterable[int], lengths: Iterable[int], chunk: in
     return out
 
 
-def frames_verify(stream_buf, frame_offsets, crc_out=None, stream=None):
-    """Verify n wire frames (rpc.h header + body) in a device byte tensor -> (ok uint8, crc int32)."""
+def _frames_flags(role: str, lift_cap: bool) -> int:
+    try:
+        f = {"server": FRAMES_SERVER, "client": FRAMES_CLIENT}[role]
+    except KeyError:
+        raise ValueError("role must be 'server' (PING is control) or 'client' (PONG is control)") from None
+    return f | (FRAMES_LIFT_CAP if lift_cap else 0)
+
+
+def frames_verify(stream_buf, frame_offsets, role: str = "server", lift_cap: bool = False, stream_bytes=None,
+                  crc_out=None, stream=None):
+    """Verify n wire frames (rpc.h header + body) in a device byte tensor.
+
+    Returns (verdict uint8 tensor of FRAME_*, crc int32 tensor).  ``role`` picks the
+    heartbeat that is a control frame: "server" -> PING (rpc_server_main.c:172),
+    "client" -> PONG (rpc_async.c:303).  Without ``lift_cap`` a data frame whose
+    body_len exceeds MAX_BODY_LEN is FRAME_TOO_LARGE (rpc_server_main.c:189)."""
     t = _torch()
     n = frame_offsets.numel()
-    ok = t.empty(n, dtype=t.uint8, device=stream_buf.device)
+    nbytes = stream_buf.numel() * stream_buf.element_size() if stream_bytes is None else int(stream_bytes)
+    verdict = t.empty(n, dtype=t.uint8, device=stream_buf.device)
     crc = _dev_u32_out(n, stream_buf.device, crc_out)
-    check(_lib.rpc_frames_verify_device(stream_buf.data_ptr(), frame_offsets.data_ptr(), n, ok.data_ptr(),
-                                        crc.data_ptr(), _stream_handle(stream)), "rpc_frames_verify_device")
-    return ok, crc
+    check(_lib.rpc_frames_verify_device(stream_buf.data_ptr(), nbytes, frame_offsets.data_ptr(), n,
+                                        _frames_flags(role, lift_cap), verdict.data_ptr(), crc.data_ptr(),
+                                        _stream_handle(stream)), "rpc_frames_verify_device")
+    return verdict, crc
 
 
-def frames_stamp(stream_buf, frame_offsets, body_lens, version: int = 1, type_: int = RPC_TYPE_DATA, stream=None):
-    """Write rpc.h headers (BE version/type/body_len/crc32) in front of device-resident bodies."""
+def frames_stamp(stream_buf, frame_offsets, body_lens, version: int = 1, type_: int = RPC_TYPE_DATA,
+                 lift_cap: bool = False, stream_bytes=None, stream=None):
+    """Write rpc.h headers (BE version/type/body_len/crc32) in front of device-resident
+    bodies; returns the per-frame verdict (FRAME_OK stamped, FRAME_TOO_LARGE /
+    FRAME_MALFORMED not stamped)."""
+    t = _torch()
     n = frame_offsets.numel()
-    check(_lib.rpc_frames_stamp_device(stream_buf.data_ptr(), frame_offsets.data_ptr(), body_lens.data_ptr(), n,
-                                       version, type_, _stream_handle(stream)), "rpc_frames_stamp_device")
+    nbytes = stream_buf.numel() * stream_buf.element_size() if stream_bytes is None else int(stream_bytes)
+    verdict = t.empty(n, dtype=t.uint8, device=stream_buf.device)
+    check(_lib.rpc_frames_stamp_device(stream_buf.data_ptr(), nbytes, frame_offsets.data_ptr(), body_lens.data_ptr(),
+                                       n, version, type_, FRAMES_LIFT_CAP if lift_cap else 0, verdict.data_ptr(),
+                                       _stream_handle(stream)), "rpc_frames_stamp_device")
+    return verdict
 
 
 def fill_random(tensor, seed: int, stream=None):
@@ -225,7 +266,7 @@ RAGGED_PATHS = {"auto": 0, "rows": 1, "packed": 2, "split": 3}
 
 
 def set_ragged_path(path="auto"):
-    """Kernel for ragged device batches: "auto" (frames: packed, other batches: rows),
+    """Kernel for ragged device batches: "auto" (frames: split, other batches: rows),
     "rows" (one wavefront per body), "packed" (1 KiB chunks of consecutive
     bodies, four per row) or "split" (bodies <= 1 KiB four per row, the rest
     one wavefront per body)."""

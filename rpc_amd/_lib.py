@@ -52,11 +52,11 @@ rpc_crc32_verify_batch = _sig("rpc_crc32_verify_batch", ctypes.c_int64, _u8p, _v
 rpc_crc32_device_batch = _sig("rpc_crc32_device_batch", _i32, _vp, _vp, _vp, _u64, _vp, _vp)
 rpc_crc32_device_uniform = _sig("rpc_crc32_device_uniform", _i32, _vp, _u64, _u32, _u64, _vp, _vp)
 rpc_crc32_device_large = _sig("rpc_crc32_device_large", _i32, _vp, _vp, _vp, _u64, _vp, _u64, _vp)
-rpc_frames_verify_device = _sig("rpc_frames_verify_device", _i32, _vp, _vp, _u64, _vp, _vp, _vp)
+rpc_frames_verify_device = _sig("rpc_frames_verify_device", _i32, _vp, _u64, _vp, _u64, _i32, _vp, _vp, _vp)
 rpc_frames_stamp_device = _sig(
-    "rpc_frames_stamp_device", _i32, _vp, _vp, _vp, _u64, ctypes.c_uint16, ctypes.c_uint16, _vp
+    "rpc_frames_stamp_device", _i32, _vp, _u64, _vp, _vp, _u64, ctypes.c_uint16, ctypes.c_uint16, _i32, _vp, _vp
 )
-rpc_rx_ring_create = _sig("rpc_rx_ring_create", _i32, ctypes.POINTER(ctypes.c_void_p), _sz, _sz, _i32)
+rpc_rx_ring_create = _sig("rpc_rx_ring_create", _i32, ctypes.POINTER(ctypes.c_void_p), _sz, _sz, _i32, _i32)
 rpc_rx_ring_destroy = _sig("rpc_rx_ring_destroy", None, _vp)
 rpc_rx_ring_reserve = _sig("rpc_rx_ring_reserve", _i32, _vp, _sz, ctypes.POINTER(ctypes.c_void_p))
 rpc_rx_ring_commit = _sig("rpc_rx_ring_commit", _i32, _vp, _u64)
@@ -102,7 +102,7 @@ class RxFrame(ctypes.Structure):
     """rpc_rx_frame_t (include/rpccrc.h)."""
     _fields_ = [("tag", ctypes.c_uint64), ("frame", ctypes.c_void_p), ("body_len", ctypes.c_uint32),
                 ("version", ctypes.c_uint16), ("type", ctypes.c_uint16), ("header_crc", ctypes.c_uint32),
-                ("crc", ctypes.c_uint32), ("ok", ctypes.c_uint8)]
+                ("crc", ctypes.c_uint32), ("ok", ctypes.c_uint8), ("verdict", ctypes.c_uint8)]
 
 
 rpc_rx_ring_poll = _sig("rpc_rx_ring_poll", ctypes.c_int64, _vp, ctypes.POINTER(RxFrame), _sz, _i32)

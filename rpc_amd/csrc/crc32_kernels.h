@@ -28,7 +28,40 @@ struct ItemsArgs {
   // item i's CRC goes to out[out_idx[i]].
   const uint64_t *n_dev = nullptr;
   const uint32_t *out_idx = nullptr;
+  // Big-body route (QB = 1 ragged only): a body with length >= big_min whose
+  // bit is set in `routed` (indexed by its batch index, out_idx[i] or i) is
+  // taken as empty here; launch_big_route computes its CRC afterwards.
+  const uint32_t *routed = nullptr;
+  uint32_t big_min = 0xFFFFFFFFu;
 };
+
+// ---- big bodies of a ragged batch ----------------------------
+// One wave per body would leave a long body streaming through a single wave
+// while the rest of the chip idles.  Bodies of >= kBigMin bytes (up to
+// kBigMaxBodies per batch; any further ones keep one wave each) are cut into
+// chunks on the device, CRC'd by the rows kernel (RAW) and folded per body.
+constexpr uint32_t kBigMin = 256u << 10;
+constexpr uint32_t kBigMaxBodies = 16384;
+constexpr uint64_t kBigMaxChunks = 1ull << 20;
+constexpr uint64_t kBigMinChunk = 16384; // power of two; grows so the chunks fit kBigMaxChunks
+struct BigRoute {
+  uint32_t *routed;  // bit i: body i takes the route (ceil(n / 64) * 2 words, all written)
+  uint64_t *meta;    // [0] bodies claimed, [1] their bytes, [2] chunks, [3] chunk bytes
+  uint32_t *b_idx;   // kBigMaxBodies: batch index of each routed body
+  uint64_t *b_first; // kBigMaxBodies + 1: first chunk of each routed body
+  uint64_t *c_off;   // kBigMaxChunks: chunk offsets / lengths / crc0
+  uint32_t *c_len;
+  uint32_t *c_raw;
+};
+size_t big_route_workspace_bytes(uint64_t n);
+BigRoute big_route_carve(void *ws, uint64_t n);
+// Before the rows pass: flags and lists the big bodies (route.routed goes into
+// the rows pass's ItemsArgs).  Stream-ordered, no host round trip.
+hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, const BigRoute &r, hipStream_t s);
+// After the rows pass: chunk plan, chunk CRCs (rows kernel, RAW), per-body
+// fold into out[batch index].
+hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,
+                            hipStream_t s);
 
 constexpr uint32_t kShiftNibWords = 64u * 8u * 16u; // 32 KiB: the chunk combine's shift maps
 

@@ -436,6 +436,205 @@ hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes,
   return launch_rows(a, 1, nt, max_blocks, s);
 }
 
+// ---------------------------------------------------------------------------
+// Big bodies of a ragged batch (crc32_kernels.h BigRoute): a
+// classify pass before the rows pass claims up to kBigMaxBodies bodies of
+// >= kBigMin bytes (the rows pass then takes them as empty), and after it a
+// one-block plan picks a power-of-two chunk so the chunks fit kBigMaxChunks,
+// an expand pass writes the chunk table, the rows kernel CRCs the chunks
+// (RAW) and a persistent combine folds them per body.  Every count stays on
+// the device; the host only launches.
+// ---------------------------------------------------------------------------
+namespace {
+
+__global__ void __launch_bounds__(256) big_classify_kernel(const uint32_t *lengths, uint64_t n, BigRoute r) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t len = (i < n) ? lengths[i] : 0u;
+  const bool big = i < n && len >= kBigMin;
+  const uint64_t m = __builtin_amdgcn_ballot_w64(big);
+  uint64_t routed = 0;
+  if (m != 0) { // wave-uniform: one slot claim per wave
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(reinterpret_cast<unsigned long long *>(&r.meta[0]), (unsigned long long)__popcll(m));
+    base = __shfl(base, 0, 64);
+    const uint64_t slot = base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+    const bool take = big && slot < kBigMaxBodies;
+    if (take) {
+      r.b_idx[slot] = (uint32_t)i;
+      atomicAdd(reinterpret_cast<unsigned long long *>(&r.meta[1]), (unsigned long long)len);
+    }
+    routed = __builtin_amdgcn_ballot_w64(take);
+  }
+  const uint64_t w0 = i - lane; // the wave's first item (a multiple of 64): its two bitmap words
+  if (w0 < n) {
+    if (lane == 0) r.routed[w0 >> 5] = (uint32_t)routed;
+    if (lane == 32) r.routed[(w0 >> 5) + 1] = (uint32_t)(routed >> 32);
+  }
+}
+
+__device__ __forceinline__ uint64_t big_count(const BigRoute &r) {
+  const uint64_t c = r.meta[0];
+  return c < kBigMaxBodies ? c : kBigMaxBodies;
+}
+
+// One block: chunk size, per-body chunk counts and their exclusive scan.
+__global__ void __launch_bounds__(1024) big_plan_kernel(const uint32_t *lengths, BigRoute r) {
+  __shared__ unsigned long long wsum[16];
+  __shared__ unsigned long long run;
+  const uint64_t nb = big_count(r);
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  if (nb == 0) {
+    if (t == 0) {
+      r.meta[2] = 0;
+      r.meta[3] = kBigMinChunk;
+    }
+    return;
+  }
+  uint64_t chunk = kBigMinChunk; // sum ceil(len / chunk) <= bytes / chunk + 1 + nb
+  while (r.meta[1] / chunk + 1 + nb > kBigMaxChunks) chunk <<= 1;
+  if (t == 0) run = 0;
+  __syncthreads();
+  for (uint64_t base = 0; base < nb; base += 1024) {
+    const uint64_t b = base + t;
+    const unsigned long long c = (b < nb) ? ((uint64_t)lengths[r.b_idx[b]] + chunk - 1) / chunk : 0ull;
+    unsigned long long x = c; // inclusive wave scan
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    unsigned long long pre = run;
+    for (uint32_t k = 0; k < w; ++k) pre += wsum[k];
+    if (b < nb) r.b_first[b] = pre + x - c;
+    __syncthreads();
+    if (t == 1023) run = pre + x;
+    __syncthreads();
+  }
+  if (t == 0) {
+    r.b_first[nb] = run;
+    r.meta[2] = run;
+    r.meta[3] = chunk;
+  }
+}
+
+// Chunk table: end-aligned chunks of each routed body (the first one partial).
+__global__ void __launch_bounds__(256) big_expand_kernel(const uint64_t *offsets, const uint32_t *lengths, BigRoute r) {
+  const uint64_t total = r.meta[2], nb = big_count(r), chunk = r.meta[3];
+  for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256u) {
+    uint64_t lo = 0, hi = nb; // last body with b_first <= t (every body has >= 1 chunk)
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (r.b_first[mid] <= t) lo = mid; else hi = mid;
+    }
+    const uint32_t i = r.b_idx[lo];
+    const uint64_t L = lengths[i], nch = r.b_first[lo + 1] - r.b_first[lo], k = t - r.b_first[lo];
+    const uint64_t end = L - (nch - 1 - k) * chunk;
+    const uint64_t start = end > chunk ? end - chunk : 0;
+    r.c_off[t] = offsets[i] + start;
+    r.c_len[t] = (uint32_t)(end - start);
+  }
+}
+
+// Persistent fold: block b takes routed bodies b, b + grid, ...: thread t runs
+// Horner over chunks t, t + 1024, ... with the step map A_{1024 * chunk} (one
+// nibble map: chunk is a power of two), shifts its partial to the body end,
+// and the block XOR-reduces: crc = ~(A_L(F) ^ XOR_k A_{(nch-1-k) chunk}(raw_k)).
+__global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengths, BigRoute r, const uint4 *shift_nib,
+                                                           uint32_t *out) {
+  __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
+  __shared__ uint32_t part[16];
+  const uint64_t nb = big_count(r);
+  if (blockIdx.x >= nb) return;
+  const uint32_t t = threadIdx.x;
+  {
+    uint4 *dst = reinterpret_cast<uint4 *>(nib);
+#pragma unroll
+    for (uint32_t q = 0; q < kShiftNibWords / 4 / 1024; ++q) dst[q * 1024 + t] = shift_nib[q * 1024 + t];
+  }
+  __syncthreads();
+  const uint64_t chunk = r.meta[3], step = 1024ull * chunk;
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t i = r.b_idx[b];
+    const uint64_t L = lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first;
+    uint32_t acc = 0;
+    for (uint64_t k = t; k < nch; k += 1024) acc = nib_shift(nib, step, acc) ^ r.c_raw[first + k];
+    if (t < nch) {
+      const uint64_t kl = t + (nch - 1 - t) / 1024 * 1024;
+      acc = nib_shift(nib, (nch - 1 - kl) * chunk, acc);
+    }
+    for (int m = 1; m < 64; m <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, m, 64);
+    if ((t & 63u) == 0) part[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) {
+      for (uint32_t w = 1; w < 16; ++w) acc ^= part[w];
+      out[i] = acc ^ ~nib_shift(nib, L, 0xFFFFFFFFu);
+    }
+    __syncthreads();
+  }
+}
+
+} // namespace
+
+size_t big_route_workspace_bytes(uint64_t n) {
+  return align256((n + 63) / 64 * 8) + align256(32) + align256(kBigMaxBodies * 4) +
+         align256((kBigMaxBodies + 1) * 8) + align256(kBigMaxChunks * 8) + 2 * align256(kBigMaxChunks * 4);
+}
+
+BigRoute big_route_carve(void *ws, uint64_t n) {
+  uint8_t *w = static_cast<uint8_t *>(ws);
+  auto take = [&](size_t bytes) {
+    uint8_t *p = w;
+    w += align256(bytes);
+    return p;
+  };
+  BigRoute r;
+  r.routed = reinterpret_cast<uint32_t *>(take((n + 63) / 64 * 8));
+  r.meta = reinterpret_cast<uint64_t *>(take(32));
+  r.b_idx = reinterpret_cast<uint32_t *>(take(kBigMaxBodies * 4));
+  r.b_first = reinterpret_cast<uint64_t *>(take((kBigMaxBodies + 1) * 8));
+  r.c_off = reinterpret_cast<uint64_t *>(take(kBigMaxChunks * 8));
+  r.c_len = reinterpret_cast<uint32_t *>(take(kBigMaxChunks * 4));
+  r.c_raw = reinterpret_cast<uint32_t *>(take(kBigMaxChunks * 4));
+  return r;
+}
+
+hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, const BigRoute &r, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n >= 0xFFFFFFFFull) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(r.meta, 0, 32, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(big_classify_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lengths, n, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,
+                            hipStream_t s) {
+  if (proto.n_items == 0) return hipSuccess;
+  if (proto.mode != kModeFinal || proto.offsets == nullptr || proto.lengths == nullptr) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(big_plan_kernel, dim3(1), dim3(1024), 0, s, proto.lengths, r);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(big_expand_kernel, dim3(512), dim3(256), 0, s, proto.offsets, proto.lengths, r);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  ItemsArgs a = proto; // the chunks: rows kernel, RAW, count on the device
+  a.offsets = r.c_off;
+  a.lengths = r.c_len;
+  a.n_items = kBigMaxChunks;
+  a.n_dev = r.meta + 2;
+  a.out_idx = nullptr;
+  a.routed = nullptr;
+  a.big_min = 0xFFFFFFFFu;
+  a.mode = kModeRaw;
+  a.out = r.c_raw;
+  e = launch_rows(a, 1, nt, max_blocks, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(big_combine_kernel, dim3(256), dim3(1024), 0, s, proto.lengths, r, shift_nib, proto.out);
+  return hipGetLastError();
+}
+
 hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream) {
   if (nbytes == 0) return hipSuccess;
   if (nbytes % 8 != 0) return hipErrorInvalidValue;

@@ -1,6 +1,6 @@
-// rpc_amd/csrc/crc32_layout.h -- LDS table image layout of the batched kernel.
+// rpc_amd/csrc/crc32_layout.h -- LDS table image layout of the rows kernel.
 //
-// One persistent 1024-thread workgroup per CU owns 156 KiB of LDS holding every
+// One persistent 1024-thread workgroup per CU owns 155 KiB of LDS holding every
 // table the kernel looks up.  All lookups are ds_read_b32 whose bank is
 // (byte_addr/4) mod 32 (MI355X_MICROARCH.md, LDS table): a table replicated 32
 // times with copy c = lane & 31 at bank c is conflict-free for ANY indices.
@@ -9,33 +9,17 @@
 //                        256-byte row so that one v_perm_b32 forms the address:
 //                        region 0: row v = { T3[v] x32 | T2[v] x32 }
 //                        region 1: row v = { T1[v] x32 | T0[v] x32 } (+64 KiB)
-//   S1     16 KiB        per-lane shift, step 1 (nibble tables, 32 copies):
-//                        S1[n][nib][c] = A_{64*(7-(c&7))}(nib << 4n)
-//   S2     4 KiB         per-lane shift, step 2 (nibble tables, 8 groups):
-//                        S2[n][nib][h] = A_{512*(G/8-1-(h & (G/8-1)))}(nib << 4n)
-//   RW     512 B         row Horner step: RW[n][nib] = A_{ROW}(nib << 4n)
-//   ZI     7.5 KiB       trailing-pad undo: ZI[z-1][n][nib] = A_z^-1(nib << 4n)
-//
-// ROW = 64 lanes-per-group(G) * 64 bytes-per-lane-segment; G in {16, 64}.
+//   then the shift tables listed below (ST1, ST2, RW, ZI, TQ16).
 #pragma once
 #include <stdint.h>
 
 namespace rpccrc {
 
-constexpr uint32_t kSegBytes = 64;           // bytes per lane per row
 constexpr uint32_t kLdsMain = 0;
 constexpr uint32_t kLdsMainRegion1 = 65536;
-constexpr uint32_t kLdsS1 = 131072;
-constexpr uint32_t kLdsS2 = kLdsS1 + 16384;  // 147456
-constexpr uint32_t kLdsRW = kLdsS2 + 4096;   // 151552
-constexpr uint32_t kLdsZI = kLdsRW + 512;    // 152064
-constexpr uint32_t kLdsBytes = kLdsZI + 15 * 512; // 159744 (156 KiB), v1 image
-constexpr uint32_t kLdsBytesV2 = 158736;          // rows-kernel image (155 KiB)
-constexpr uint32_t kLdsWords = kLdsBytes / 4;
-constexpr uint32_t kMaxRow = 64 * kSegBytes; // 4096
+constexpr uint32_t kLdsBytesV2 = 158736;     // rows-kernel image (155 KiB)
+constexpr uint32_t kMaxRow = 4096;           // 64 lanes x 64-byte segments
 constexpr uint32_t kTqEntries = kMaxRow + 1; // Tq[q] = A_q(0xFFFFFFFF), q=0..4096
-
-constexpr uint32_t row_bytes(int G) { return (uint32_t)G * kSegBytes; }
 
 // ---- rows-kernel image (crc32_rows.h): main tables as above, then
 //   ST1 16 KiB  A_{64*(15-(c&15))}(nib << 4n), c = lane & 31, at
@@ -59,8 +43,7 @@ static_assert(kLdsTQ16 + 1040 == kLdsBytesV2, "rows image size");
 static_assert(kLdsBytesV2 % 16 == 0 && kLdsBytesV2 <= 163840, "fits the 160 KiB LDS");
 void build_lds_image_v2(uint32_t *img /* kLdsBytesV2 bytes */);
 
-// Host-side builders (crc32_tables.cpp).
-void build_lds_image(int G, uint32_t *img /* kLdsWords */);
+// Host-side builder (crc32_tables.cpp).
 void build_tq(uint32_t *tq /* kTqEntries */);
 
 } // namespace rpccrc

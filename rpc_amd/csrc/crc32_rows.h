@@ -395,6 +395,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if (threadIdx.x <= 2 * kDynSlots)
       s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots : 0u;
   }
+  // Device-side item counts (split lists, big-body chunks) may be 0: leave
+  // before the 155 KiB image copy (block-uniform).
+  if (a.n_dev != nullptr && ld_const(a.n_dev, 0) == 0) return;
   uint64_t t_entry = 0, t_image = 0;
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   // All of this thread's image loads in flight at once (a rolled loop would
@@ -494,6 +497,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
                     uint32_t &seed) {
       const uint64_t off = RAGGED ? ld_const(a.offsets, item) : item * a.stride;
       len = RAGGED ? ld_const(a.lengths, item) : a.len;
+      if constexpr (RAGGED) {
+        // a routed big body is empty here (launch_big_route computes it)
+        if (len >= a.big_min && a.routed != nullptr) {
+          const uint64_t bi = a.out_idx ? (uint64_t)ld_const(a.out_idx, item) : item;
+          if ((ld_const(a.routed, bi >> 5) >> (bi & 31u)) & 1u) len = 0;
+        }
+      }
       p0 = (uint64_t)(uintptr_t)a.base + off;
       z = (uint32_t)(0u - (uint32_t)(p0 + len)) & 15u;
       lp = (uint64_t)len + z;

@@ -22,52 +22,6 @@ void nibble_table_inverse(uint32_t nbytes, uint32_t out[8][16]) {
 }
 } // namespace
 
-void build_lds_image(int G, uint32_t *img) {
-  memset(img, 0, kLdsBytes);
-  uint8_t *b = reinterpret_cast<uint8_t *>(img);
-  auto put = [&](uint32_t byte_addr, uint32_t v) { memcpy(b + byte_addr, &v, 4); };
-
-  // MAIN: slice-by-4 tables, 32 copies, 2 tables per 256-byte row.
-  for (uint32_t v = 0; v < 256; ++v) {
-    const uint32_t t0 = crc_slice_entry(0, v), t1 = crc_slice_entry(1, v);
-    const uint32_t t2 = crc_slice_entry(2, v), t3 = crc_slice_entry(3, v);
-    for (uint32_t c = 0; c < 32; ++c) {
-      put(kLdsMain + v * 256 + c * 4, t3);
-      put(kLdsMain + v * 256 + 128 + c * 4, t2);
-      put(kLdsMainRegion1 + v * 256 + c * 4, t1);
-      put(kLdsMainRegion1 + v * 256 + 128 + c * 4, t0);
-    }
-  }
-  // S1: per-lane shift by 64*(7-(lane&7)) bytes, 32 copies (c = lane & 31).
-  uint32_t nt[8][16];
-  for (uint32_t c = 0; c < 32; ++c) {
-    nibble_table(kSegBytes * (7u - (c & 7u)), nt);
-    for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib)
-        put(kLdsS1 + n * 2048 + nib * 128 + c * 4, nt[n][nib]);
-  }
-  // S2: per-group shift by 512*(G/8-1-(h & (G/8-1))) bytes, h = lane >> 3.
-  const uint32_t groups8 = (uint32_t)G / 8;
-  for (uint32_t h = 0; h < 8; ++h) {
-    nibble_table(8 * kSegBytes * (groups8 - 1 - (h & (groups8 - 1))), nt);
-    for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib)
-        put(kLdsS2 + n * 512 + nib * 32 + h * 4, nt[n][nib]);
-  }
-  // RW: one full row.
-  nibble_table(row_bytes(G), nt);
-  for (int n = 0; n < 8; ++n)
-    for (uint32_t nib = 0; nib < 16; ++nib)
-      put(kLdsRW + n * 64 + nib * 4, nt[n][nib]);
-  // ZI: undo z = 1..15 trailing zero bytes.
-  for (uint32_t z = 1; z <= 15; ++z) {
-    nibble_table_inverse(z, nt);
-    for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib)
-        put(kLdsZI + (z - 1) * 512 + n * 64 + nib * 4, nt[n][nib]);
-  }
-}
-
 void build_lds_image_v2(uint32_t *img) {
   memset(img, 0, kLdsBytesV2);
   uint8_t *b = reinterpret_cast<uint8_t *>(img);

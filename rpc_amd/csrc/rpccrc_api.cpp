@@ -1,11 +1,18 @@
 // rpc_amd/csrc/rpccrc_api.cpp -- C-ABI host layer of librpccrc (include/rpccrc.h).
 //
-// Owns per-device state (table images in HBM, built once per device with
-// std::call_once so the drop-in calls stay thread-safe without an init call,
-// SURVEY.md 8b "Threading"), per-thread staging for the drop-in scalar path, and
-// the host-buffer pipeline of rpc_crc32_batch.  Every CRC value this library
-// returns is computed by the HIP kernels in crc32_kernels.hip / frames.hip;
-// there is no CPU CRC implementation in the product path.
+// Owns per-device state, built once per device with std::call_once so the
+// drop-in calls stay thread-safe without an init call (SURVEY.md 8b
+// "Threading"):
+//  * the table images in HBM;
+//  * pools that lend resources to one call at a time and take them back when
+//    the call returns -- device workspaces and pinned staging (BlockPool), the
+//    drop-in scalar path's streams and staging (ScalarCtx), the host-batch
+//    pipelines (HostPipeline).  Nothing is per thread, so a thread-per-
+//    connection server that exits threads leaks nothing, and the memory held
+//    is bounded by the peak number of concurrent calls.
+// Every CRC value this library returns is computed by the HIP kernels in
+// crc32_kernels.hip / frames.hip; there is no CPU CRC implementation in the
+// product path.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -14,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -28,23 +36,211 @@ namespace {
 
 constexpr int kMaxDevices = 64;
 
+int map_hip(hipError_t e) {
+  if (e == hipSuccess) return RPCCRC_OK;
+  if (e == hipErrorOutOfMemory) return RPCCRC_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return RPCCRC_ENODEV;
+  if (e == hipErrorInvalidValue) return RPCCRC_EINVAL;
+  return RPCCRC_EIO;
+}
+
+#define RPCCRC_TRY(expr)                      \
+  do {                                        \
+    const hipError_t _e = (expr);             \
+    if (_e != hipSuccess) return map_hip(_e); \
+  } while (0)
+
+// ---- pools -----------------------------------------------------------------
+
+// A cached block of device memory (or pinned host memory) lent to one call at
+// a time.  `ev` is recorded on the stream of the block's last use when the
+// call returns it.  The next borrower orders itself after that use: a device
+// block through hipStreamWaitEvent on its own stream (no host wait, and valid
+// even if the earlier stream has been destroyed since -- the event outlives
+// it), a pinned block through hipEventSynchronize (the host is about to write
+// it).  Replaces per-call hipMallocAsync/hipFreeAsync, whose free blocked the
+// calling thread until the GPU reached it (profiles/r01h_*), and the r01
+// per-thread cache that hipFree'd on every stream switch.
+struct Block {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool used = false;
+};
+
+class BlockPool {
+ public:
+  BlockPool(bool pinned, size_t keep) : pinned_(pinned), keep_(keep) {}
+
+  int acquire(size_t bytes, hipStream_t s, Block *out) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      int best = -1;
+      for (int i = 0; i < (int)free_.size(); ++i)
+        if (free_[i].cap >= bytes && (best < 0 || free_[i].cap < free_[best].cap)) best = i;
+      if (best >= 0) {
+        *out = free_[best];
+        free_.erase(free_.begin() + best);
+        cached_ -= out->cap;
+      }
+    }
+    if (out->p) {
+      if (out->used) RPCCRC_TRY(pinned_ ? hipEventSynchronize(out->ev) : hipStreamWaitEvent(s, out->ev, 0));
+      return RPCCRC_OK;
+    }
+    size_t cap = pinned_ ? (64u << 10) : (1u << 20);
+    while (cap < bytes) cap <<= 1;
+    Block b;
+    hipError_t e = pinned_ ? hipHostMalloc(&b.p, cap, hipHostMallocDefault) : hipMalloc(&b.p, cap);
+    if (e != hipSuccess) {
+      b.p = nullptr;
+      return map_hip(e);
+    }
+    e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      (void)(pinned_ ? hipHostFree(b.p) : hipFree(b.p));
+      return map_hip(e);
+    }
+    b.cap = cap;
+    *out = b;
+    return RPCCRC_OK;
+  }
+
+  // Returns the block after the call has enqueued its last use on stream s.
+  void release(Block &b, hipStream_t s) {
+    if (!b.p) return;
+    b.used = hipEventRecord(b.ev, s) == hipSuccess;
+    if (!b.used) (void)hipStreamSynchronize(s); // no event: make the block idle now
+    std::vector<Block> evict;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      free_.push_back(b);
+      cached_ += b.cap;
+      // Over the keep limit: drop the largest idle blocks (rare; e.g. after a
+      // one-off huge batch).
+      while (cached_ > keep_ && !free_.empty()) {
+        auto it = std::max_element(free_.begin(), free_.end(),
+                                   [](const Block &x, const Block &y) { return x.cap < y.cap; });
+        cached_ -= it->cap;
+        evict.push_back(*it);
+        free_.erase(it);
+      }
+    }
+    for (Block &x : evict) {
+      if (x.used) (void)hipEventSynchronize(x.ev);
+      (void)(pinned_ ? hipHostFree(x.p) : hipFree(x.p));
+      (void)hipEventDestroy(x.ev);
+    }
+    b = Block();
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<Block> free_;
+  size_t cached_ = 0;
+  const bool pinned_;
+  const size_t keep_;
+};
+
+// A block borrowed for the duration of one call (returned by the destructor,
+// after the call has enqueued all its work on `s`).
+struct Lease {
+  BlockPool *pool = nullptr;
+  Block b;
+  hipStream_t s = nullptr;
+  Lease() = default;
+  Lease(const Lease &) = delete;
+  Lease &operator=(const Lease &) = delete;
+  ~Lease() {
+    if (pool) pool->release(b, s);
+  }
+  int get(BlockPool *p, size_t bytes, hipStream_t stream) {
+    pool = p;
+    s = stream;
+    return p->acquire(bytes, stream, &b);
+  }
+  uint8_t *ptr() const { return static_cast<uint8_t *>(b.p); }
+};
+
+// A simple free list of T (one borrower at a time, created on demand).
+template <class T>
+class ObjPool {
+ public:
+  T *acquire() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!free_.empty()) {
+        T *t = free_.back();
+        free_.pop_back();
+        return t;
+      }
+    }
+    return new T();
+  }
+  void release(T *t) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(t);
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<T *> free_;
+};
+
+// Drop-in scalar path: a non-blocking stream plus pinned staging.
+struct ScalarCtx {
+  hipStream_t stream = nullptr;
+  uint8_t *pin = nullptr;   // pinned input staging, device-readable (zero-copy)
+  uint32_t *pout = nullptr; // pinned result
+  uint8_t *dbuf = nullptr;  // device staging for large bodies
+  size_t dcap = 0;
+};
+
+// rpc_crc32_batch: two slots, each a stream with a device stage and pinned
+// metadata, so one group's H2D overlaps the previous group's kernel.
+constexpr uint64_t kStageBytes = 256ull << 20; // device staging per pipeline slot
+constexpr uint64_t kStageMaxBodies = 1ull << 20;
+struct HostSlot {
+  hipStream_t stream = nullptr;
+  uint8_t *dbuf = nullptr;  // device copy of the group's span
+  uint64_t *doff = nullptr; // rebased offsets
+  uint32_t *dlen = nullptr;
+  uint32_t *dout = nullptr;
+  uint64_t *hoff = nullptr; // pinned staging for metadata
+  uint32_t *hlen = nullptr;
+  uint32_t *hout = nullptr;
+  uint64_t first = 0, count = 0; // bodies of the group in flight
+  bool busy = false;
+};
+struct HostPipeline {
+  HostSlot slot[2];
+  bool ok = false;
+};
+
 struct DeviceCtx {
   int device = -1;
   int cus = 0;
-  uint4 *img = nullptr;   // LDS table image (v2 layout, 160 KiB)
+  uint4 *img = nullptr; // LDS table image (rows kernel layout, 155 KiB)
   uint32_t *tq = nullptr;
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
   int status = RPCCRC_ENODEV;
   char name[128] = {0};
   char arch[64] = {0};
+  // Pools (never destroyed: a static destructor would run after the HIP
+  // runtime's own teardown; the process exit releases everything).
+  BlockPool *ws = nullptr;  // device workspaces (keeps <= 1 GiB idle)
+  BlockPool *pin = nullptr; // pinned staging (keeps <= 256 MiB idle)
+  ObjPool<ScalarCtx> *scalar = nullptr;
+  ObjPool<HostPipeline> *pipes = nullptr;
 };
 
 DeviceCtx g_dev[kMaxDevices];
 std::once_flag g_once[kMaxDevices];
 
-int g_nontemporal = 1; // streamed once: non-temporal loads (measured faster)
-int g_max_blocks = 0;
-int g_ragged_path = RPCCRC_RAGGED_AUTO;
+// Process-wide knobs (written by rpc_crc32_set_*, read by every call).
+std::atomic<int> g_nontemporal{1}; // streamed once: non-temporal loads (measured faster)
+std::atomic<int> g_max_blocks{0};
+std::atomic<int> g_ragged_path{RPCCRC_RAGGED_AUTO};
 // Large-body chunk (rpc_crc32_device_large, chunk_bytes = 0).  C4 per call
 // (profiles/r01c4_*): 4 KiB 697 us (rows kernel fastest, combine 27 us),
 // 16 KiB 673 us, 64 KiB 689 us (each wave streams its own 64 KiB).
@@ -54,6 +250,7 @@ const uint64_t g_large_chunk = [] {
   const unsigned long long v = e ? strtoull(e, nullptr, 10) : 0ull;
   return (v >= 16 && v % 16 == 0 && v <= (1ull << 31)) ? (uint64_t)v : (uint64_t)16384;
 }();
+const bool g_large_chunk_env = getenv("RPCCRC_LARGE_CHUNK") != nullptr;
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kPackedMinBodies = 64;         // fewer frames: one wave per body (rows kernel)
 constexpr bool kAutoSplitFrames = true;           // AUTO frames batches: split (true) or packed (false)
@@ -68,20 +265,6 @@ uint64_t packed_min_slice() {
   }();
   return v;
 }
-
-int map_hip(hipError_t e) {
-  if (e == hipSuccess) return RPCCRC_OK;
-  if (e == hipErrorOutOfMemory) return RPCCRC_ENOMEM;
-  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return RPCCRC_ENODEV;
-  if (e == hipErrorInvalidValue) return RPCCRC_EINVAL;
-  return RPCCRC_EIO;
-}
-
-#define RPCCRC_TRY(expr)                  \
-  do {                                    \
-    const hipError_t _e = (expr);         \
-    if (_e != hipSuccess) return map_hip(_e); \
-  } while (0)
 
 void init_device(int dev) {
   DeviceCtx &c = g_dev[dev];
@@ -122,6 +305,10 @@ void init_device(int dev) {
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);
   (void)hipSetDevice(prev);
+  c.ws = new BlockPool(false, 1ull << 30);
+  c.pin = new BlockPool(true, 256ull << 20);
+  c.scalar = new ObjPool<ScalarCtx>();
+  c.pipes = new ObjPool<HostPipeline>();
   c.status = map_hip(e);
 }
 
@@ -139,12 +326,15 @@ int get_ctx(DeviceCtx **out) {
 int max_blocks_for(const DeviceCtx &c) {
   // One 1024-thread workgroup per CU (156 KiB LDS each).
   int mb = c.cus > 0 ? c.cus : 256;
-  if (g_max_blocks > 0) mb = std::min(mb * 8, g_max_blocks);
+  const int cap = g_max_blocks.load(std::memory_order_relaxed);
+  if (cap > 0) mb = std::min(mb * 8, cap);
   return mb;
 }
 
-int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
+bool nontemporal() { return g_nontemporal.load(std::memory_order_relaxed) != 0; }
+
+ItemsArgs items_args(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths,
+                     uint64_t n, uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out) {
   ItemsArgs a;
   a.base = base;
   a.offsets = offsets;
@@ -157,62 +347,76 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   a.tq = c.tq;
   a.out = out;
   a.gshift = kRowsGroupShift;
-  return map_hip(launch_rows(a, QB, g_nontemporal != 0, max_blocks_for(c), s));
+  return a;
 }
 
-// A ragged batch on the device.  AUTO: frames (bodies capped at MAX_BODY_LEN =
-// 1 KiB, rpc.h:17) take the split path (bodies <= 1 KiB four per row through
-// the QB = 4 rows kernel: 1M frames 334 us vs 481 packed, 565 rows, DESIGN.md
-// 4.2), other batches the rows kernel (one wave per body; ahead on C2's
-// 64 B - 64 KiB mix).
+int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
+  const ItemsArgs a = items_args(c, base, offsets, lengths, n, stride, len, mode, out);
+  return map_hip(launch_rows(a, QB, nontemporal(), max_blocks_for(c), s));
+}
+
+// A ragged batch on the device.
+//  * Kernel: AUTO frames (bodies capped at MAX_BODY_LEN = 1 KiB, rpc.h:17)
+//    take the split path (bodies <= 1 KiB four per row through the QB = 4
+//    rows kernel: 1M frames 334 us vs 481 packed, 565 rows),
+//    other batches the rows kernel (one wave per body; ahead on C2's
+//    64 B - 64 KiB mix).
+//  * route: bodies of >= kBigMin bytes go through the big-body chunk route
+//    (classify before, chunks + fold after) so a long body
+//    does not stream through a single wave.  Not with the packed kernel.
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-           uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies = false) {
+           uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route) {
+  const int path = g_ragged_path.load(std::memory_order_relaxed);
+  const bool nt = nontemporal();
+  const int mb = max_blocks_for(c);
   const bool fits = n < (1ull << 27); // the packed kernel's metadata window: 8-B offsets in a 1 GiB buffer range
-  const bool auto_frames = g_ragged_path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies;
-  const bool packed = fits && (g_ragged_path == RPCCRC_RAGGED_PACKED || (auto_frames && !kAutoSplitFrames));
-  const bool split = !packed && n < 0xFFFFFFFFull &&
-                     (g_ragged_path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
-  if (split) {
+  const bool auto_frames = path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies;
+  const bool packed = fits && (path == RPCCRC_RAGGED_PACKED || (auto_frames && !kAutoSplitFrames));
+  const bool split = !packed && n < 0xFFFFFFFFull && (path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
+  route = route && !packed && mode == kModeFinal && n < 0xFFFFFFFFull;
+  ItemsArgs a = items_args(c, base, offsets, lengths, n, 0, 0, mode, out);
+  if (packed) {
+    const uint64_t ms = std::min<uint64_t>(kPackedMaxSlices, std::max<uint64_t>(8192, 4 * n));
     size_t bytes = 0;
-    RPCCRC_TRY(split_workspace_bytes(n, &bytes));
-    void *ws = nullptr;
-    RPCCRC_TRY(hipMallocAsync(&ws, bytes, s));
-    ItemsArgs a;
-    a.base = base;
-    a.offsets = offsets;
-    a.lengths = lengths;
-    a.n_items = n;
-    a.mode = mode;
-    a.lds_image = c.img;
-    a.tq = c.tq;
-    a.out = out;
-    a.gshift = kRowsGroupShift;
-    const int r = map_hip(launch_split_batch(a, ws, bytes, g_nontemporal != 0, max_blocks_for(c), s));
-    (void)hipFreeAsync(ws, s);
-    return r;
+    RPCCRC_TRY(packed_workspace_bytes(n, ms, &bytes));
+    Lease ws;
+    if (const int rc = ws.get(c.ws, bytes, s)) return rc;
+    PackedBatch p;
+    p.base = base;
+    p.offsets = offsets;
+    p.lengths = lengths;
+    p.n = n;
+    p.mode = mode;
+    p.lds_image = c.img;
+    p.tq = c.tq;
+    p.out = out;
+    p.ws = ws.ptr();
+    p.ws_bytes = bytes;
+    p.max_slices = ms;
+    p.min_slice = packed_min_slice();
+    return map_hip(launch_packed_batch(p, nt, mb, s));
   }
-  if (!packed) return items(c, base, offsets, lengths, n, 0, 0, mode, out, 1, s);
-  const uint64_t ms = std::min<uint64_t>(kPackedMaxSlices, std::max<uint64_t>(8192, 4 * n));
-  size_t bytes = 0;
-  RPCCRC_TRY(packed_workspace_bytes(n, ms, &bytes));
-  void *ws = nullptr;
-  RPCCRC_TRY(hipMallocAsync(&ws, bytes, s));
-  PackedBatch p;
-  p.base = base;
-  p.offsets = offsets;
-  p.lengths = lengths;
-  p.n = n;
-  p.mode = mode;
-  p.lds_image = c.img;
-  p.tq = c.tq;
-  p.out = out;
-  p.ws = ws;
-  p.ws_bytes = bytes;
-  p.max_slices = ms;
-  p.min_slice = packed_min_slice();
-  const int r = map_hip(launch_packed_batch(p, g_nontemporal != 0, max_blocks_for(c), s));
-  (void)hipFreeAsync(ws, s);
-  return r;
+  size_t split_bytes = 0;
+  if (split) RPCCRC_TRY(split_workspace_bytes(n, &split_bytes));
+  split_bytes = (split_bytes + 255) & ~(size_t)255;
+  const size_t route_bytes = route ? big_route_workspace_bytes(n) : 0;
+  Lease ws;
+  if (split_bytes + route_bytes > 0)
+    if (const int rc = ws.get(c.ws, split_bytes + route_bytes, s)) return rc;
+  BigRoute r{};
+  if (route) {
+    r = big_route_carve(ws.ptr() + split_bytes, n);
+    RPCCRC_TRY(launch_big_classify(lengths, n, r, s));
+    a.routed = r.routed;
+    a.big_min = kBigMin;
+  }
+  if (split)
+    RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
+  else
+    RPCCRC_TRY(launch_rows(a, 1, nt, mb, s));
+  if (route) RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s));
+  return RPCCRC_OK;
 }
 
 // ---- large bodies: chunk expansion + combine --------------------------------
@@ -256,72 +460,6 @@ __global__ void expand_chunks_inline_kernel(InlineBodies bodies, uint64_t nb, ui
   expand_chunks(bodies.b, nb, chunk, total_chunks, item_off, item_len, lens, firsts, out);
 }
 
-struct PinnedStage {
-  void *ptr = nullptr;
-  size_t cap = 0;
-  hipEvent_t ready = nullptr; // last async consumer of ptr
-  bool pending = false;
-  int reserve(size_t bytes) {
-    if (pending) {
-      (void)hipEventSynchronize(ready);
-      pending = false;
-    }
-    if (bytes <= cap) return RPCCRC_OK;
-    if (ptr) (void)hipHostFree(ptr);
-    ptr = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(bytes, 1 << 16);
-    RPCCRC_TRY(hipHostMalloc(&ptr, want, hipHostMallocDefault));
-    cap = want;
-    if (!ready) RPCCRC_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-    return RPCCRC_OK;
-  }
-  void mark(hipStream_t s) {
-    (void)hipEventRecord(ready, s);
-    pending = true;
-  }
-};
-
-thread_local PinnedStage t_large_stage;
-
-// Per-thread device workspace, reused by the next call on the same stream
-// (stream order makes the reuse safe) and grown when too small.  A
-// hipFreeAsync per call blocked the calling thread until the GPU reached it
-// and left a ~6 us gap in the stream before the next call's first kernel
-// (rocprofv3 --hip-runtime-trace, profiles/r01h_*).  Released when the thread
-// switches stream or device or needs more; a thread's last workspace is kept
-// until the process ends.
-struct StreamWorkspace {
-  int dev = -1;
-  hipStream_t stream = nullptr;
-  void *p = nullptr;
-  size_t cap = 0;
-  int get(int device, hipStream_t s, size_t bytes, void **out) {
-    if (p && (dev != device || stream != s || cap < bytes)) {
-      // hipFree, not hipFreeAsync on the old stream: the caller may have
-      // destroyed that stream by now.  hipFree waits for the device, so no
-      // queued work still uses the old workspace (only on a switch or growth).
-      int cur = -1;
-      (void)hipGetDevice(&cur);
-      if (cur != dev) (void)hipSetDevice(dev);
-      (void)hipFree(p);
-      if (cur != dev) (void)hipSetDevice(cur);
-      p = nullptr;
-      cap = 0;
-    }
-    if (!p) {
-      const size_t want = std::max<size_t>(bytes, 1u << 20);
-      RPCCRC_TRY(hipMallocAsync(&p, want, s));
-      cap = want;
-      dev = device;
-      stream = s;
-    }
-    *out = p;
-    return RPCCRC_OK;
-  }
-};
-thread_local StreamWorkspace t_large_ws;
-
 // Large bodies: end-aligned chunks, CRC'd by the rows kernel in RAW mode, then
 // folded per body by the chunk combine.
 //  * Contiguous fast path: when the bodies lie back to back and every length
@@ -333,7 +471,8 @@ thread_local StreamWorkspace t_large_ws;
 //    kernel runs ragged.
 // <= 32 bodies travel in the kernel arguments; bodies of <= 64Ki chunks get
 // one 1024-thread combine block each (plain store), longer ones several
-// blocks that XOR into the zeroed output.
+// blocks that XOR into the zeroed output.  The workspace comes from the
+// device's pool (stream-ordered reuse, no free on this path).
 int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_offsets, const uint64_t *h_lengths,
                  uint64_t n, uint32_t *d_out, uint64_t chunk, hipStream_t s) {
   if (chunk % 16 != 0 || chunk > (1ull << 31)) return RPCCRC_EINVAL;
@@ -347,7 +486,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   }
   if (chunk == 0) {
     chunk = g_large_chunk;
-    if (contiguous && lens_or % chunk != 0 && !getenv("RPCCRC_LARGE_CHUNK"))
+    if (contiguous && lens_or % chunk != 0 && !g_large_chunk_env)
       for (uint64_t cand : {8192ull, 4096ull})
         if (lens_or % cand == 0) {
           chunk = cand;
@@ -359,10 +498,10 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   uint64_t total = 0, max_nch = 0;
   InlineBodies ib;
   BodyDesc *bd = ib.b;
+  Lease stage; // pinned body table for > kInlineBodies bodies
   if (!inl) {
-    const int rc = t_large_stage.reserve(n * sizeof(BodyDesc));
-    if (rc) return rc;
-    bd = static_cast<BodyDesc *>(t_large_stage.ptr);
+    if (const int rc = stage.get(c.pin, n * sizeof(BodyDesc), s)) return rc;
+    bd = reinterpret_cast<BodyDesc *>(stage.ptr());
   }
   bool multiple = true;
   for (uint64_t i = 0; i < n; ++i) {
@@ -386,13 +525,15 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   }
   const bool fast = contiguous && multiple && splits == 1;
   const size_t ws_bytes = fast ? total * 4 + 64 : n * sizeof(BodyDesc) + n * 16 + total * (8 + 4 + 4) + 64;
-  uint8_t *ws = nullptr;
-  if (const int rc = t_large_ws.get(c.device, s, ws_bytes, reinterpret_cast<void **>(&ws))) return rc;
-  int r = RPCCRC_OK;
+  Lease wsl;
+  if (const int rc = wsl.get(c.ws, ws_bytes, s)) return rc;
+  uint8_t *ws = wsl.ptr();
   uint32_t *d_raw = reinterpret_cast<uint32_t *>(ws);
   uint64_t *d_lens = nullptr, *d_firsts = nullptr;
   if (fast) {
-    r = items(c, d_base + h_offsets[0], nullptr, nullptr, total, chunk, (uint32_t)chunk, kModeRaw, d_raw, 1, s);
+    RPCCRC_TRY(launch_rows(items_args(c, d_base + h_offsets[0], nullptr, nullptr, total, chunk, (uint32_t)chunk,
+                                      kModeRaw, d_raw),
+                           1, nontemporal(), max_blocks_for(c), s));
   } else {
     BodyDesc *d_bodies = reinterpret_cast<BodyDesc *>(ws);
     d_lens = reinterpret_cast<uint64_t *>(ws + n * sizeof(BodyDesc));
@@ -400,15 +541,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     uint64_t *d_ioff = d_firsts + n;
     uint32_t *d_ilen = reinterpret_cast<uint32_t *>(d_ioff + total);
     d_raw = d_ilen + total;
-    hipError_t e = hipSuccess;
-    if (!inl) {
-      e = hipMemcpyAsync(d_bodies, bd, n * sizeof(BodyDesc), hipMemcpyHostToDevice, s);
-      t_large_stage.mark(s);
-      if (e != hipSuccess) {
-        // the workspace stays cached for the next call on this stream
-        return map_hip(e);
-      }
-    }
+    if (!inl) RPCCRC_TRY(hipMemcpyAsync(d_bodies, bd, n * sizeof(BodyDesc), hipMemcpyHostToDevice, s));
     const uint64_t threads = std::max<uint64_t>(total, n);
     const dim3 eg((unsigned)((threads + 255) / 256));
     if (inl)
@@ -417,39 +550,25 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     else
       hipLaunchKernelGGL(expand_chunks_kernel, eg, dim3(256), 0, s, d_bodies, n, chunk, total, d_ioff, d_ilen, d_lens,
                          d_firsts, d_out);
-    r = map_hip(hipGetLastError());
-    if (r == RPCCRC_OK) r = items(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw, 1, s);
+    RPCCRC_TRY(hipGetLastError());
+    RPCCRC_TRY(launch_rows(items_args(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw), 1, nontemporal(),
+                           max_blocks_for(c), s));
   }
-  if (r == RPCCRC_OK) {
-    CombineArgs ca;
-    ca.raw = d_raw;
-    ca.lengths = d_lens;
-    ca.chunk_first = d_firsts;
-    ca.shift_nib = c.shift_nib;
-    ca.n_bodies = n;
-    ca.chunk = chunk;
-    ca.out = d_out;
-    ca.splits = (uint32_t)splits;
-    ca.inline_bodies = inl;
-    if (inl) ca.bodies = ib;
-    r = map_hip(launch_chunk_combine(ca, s));
-  }
-  // the workspace stays cached for the next call on this stream (no hipFreeAsync)
-  return r;
+  CombineArgs ca;
+  ca.raw = d_raw;
+  ca.lengths = d_lens;
+  ca.chunk_first = d_firsts;
+  ca.shift_nib = c.shift_nib;
+  ca.n_bodies = n;
+  ca.chunk = chunk;
+  ca.out = d_out;
+  ca.splits = (uint32_t)splits;
+  ca.inline_bodies = inl;
+  if (inl) ca.bodies = ib;
+  return map_hip(launch_chunk_combine(ca, s));
 }
 
-// ---- per-thread staging for the drop-in scalar path --------------------------
-
-struct ScalarCtx {
-  int device = -1;
-  hipStream_t stream = nullptr;
-  uint8_t *pin = nullptr; // pinned input staging, device-readable
-  size_t cap = 0;
-  uint32_t *pout = nullptr; // pinned result
-  uint8_t *dbuf = nullptr; // device staging for large bodies
-  size_t dcap = 0;
-};
-thread_local ScalarCtx t_scalar;
+// ---- drop-in scalar path ------------------------------------------------------
 
 [[noreturn]] void die(const char *what, int rc) {
   fprintf(stderr, "rpccrc: %s failed (%s); librpccrc requires a usable HIP device and has no CPU fallback\n", what,
@@ -460,91 +579,68 @@ thread_local ScalarCtx t_scalar;
 constexpr size_t kScalarZeroCopyMax = 64 << 10;  // read straight from pinned memory
 constexpr uint64_t kScalarChunkedMin = 8 << 20;  // chunk + combine above this
 
+int scalar_ctx_init(ScalarCtx &t) {
+  if (t.stream) return RPCCRC_OK;
+  RPCCRC_TRY(hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking));
+  RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.pout), 64, hipHostMallocDefault));
+  RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.pin), kScalarZeroCopyMax, hipHostMallocDefault));
+  return RPCCRC_OK;
+}
+
+// One CRC through the GPU.  The context (stream + staging) is borrowed from
+// the device's pool for the call: concurrent callers get distinct contexts,
+// and a context is reused by the next call of any thread.
 uint32_t scalar_crc(const void *data, uint32_t len) {
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) die("device init", rc);
-  ScalarCtx &t = t_scalar;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (t.device != dev) {
-    t.device = dev;
-    if (hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking) != hipSuccess) die("stream create", RPCCRC_EIO);
-    if (hipHostMalloc(reinterpret_cast<void **>(&t.pout), 64, hipHostMallocDefault) != hipSuccess)
-      die("pinned alloc", RPCCRC_ENOMEM);
-    t.pin = nullptr;
-    t.cap = 0;
-    t.dbuf = nullptr;
-    t.dcap = 0;
-  }
+  ScalarCtx *t = c->scalar->acquire();
+  if ((rc = scalar_ctx_init(*t))) die("scalar context", rc);
   const uint8_t *src = static_cast<const uint8_t *>(data);
   if (len <= kScalarZeroCopyMax) {
-    if (t.cap < len || !t.pin) {
-      if (t.pin) (void)hipHostFree(t.pin);
-      t.cap = kScalarZeroCopyMax;
-      if (hipHostMalloc(reinterpret_cast<void **>(&t.pin), t.cap, hipHostMallocDefault) != hipSuccess)
-        die("pinned alloc", RPCCRC_ENOMEM);
-    }
-    memcpy(t.pin, src, len);
-    rc = items(*c, t.pin, nullptr, nullptr, 1, 0, len, kModeFinal, t.pout, 1, t.stream);
+    memcpy(t->pin, src, len);
+    rc = items(*c, t->pin, nullptr, nullptr, 1, 0, len, kModeFinal, t->pout, 1, t->stream);
   } else {
-    if (t.dcap < len) {
-      if (t.dbuf) (void)hipFree(t.dbuf);
-      t.dbuf = nullptr;
-      if (hipMalloc(reinterpret_cast<void **>(&t.dbuf), len) != hipSuccess) die("device alloc", RPCCRC_ENOMEM);
-      t.dcap = len;
+    if (t->dcap < len) {
+      if (t->dbuf) (void)hipFree(t->dbuf);
+      t->dbuf = nullptr;
+      t->dcap = 0;
+      if (hipMalloc(reinterpret_cast<void **>(&t->dbuf), len) != hipSuccess) die("device alloc", RPCCRC_ENOMEM);
+      t->dcap = len;
     }
-    if (hipMemcpyAsync(t.dbuf, src, len, hipMemcpyHostToDevice, t.stream) != hipSuccess) die("H2D copy", RPCCRC_EIO);
+    if (hipMemcpyAsync(t->dbuf, src, len, hipMemcpyHostToDevice, t->stream) != hipSuccess) die("H2D copy", RPCCRC_EIO);
     if (len >= kScalarChunkedMin) {
       const uint64_t off = 0, l64 = len;
-      rc = device_large(*c, t.dbuf, &off, &l64, 1, t.pout, 0, t.stream);
+      rc = device_large(*c, t->dbuf, &off, &l64, 1, t->pout, 0, t->stream);
     } else {
-      rc = items(*c, t.dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, t.pout, 1, t.stream);
+      rc = items(*c, t->dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, t->pout, 1, t->stream);
     }
   }
   if (rc) die("kernel launch", rc);
-  if (hipStreamSynchronize(t.stream) != hipSuccess) die("stream sync", RPCCRC_EIO);
-  return *t.pout;
+  if (hipStreamSynchronize(t->stream) != hipSuccess) die("stream sync", RPCCRC_EIO);
+  const uint32_t r = *t->pout;
+  if (t->dcap > (64u << 20)) { // do not keep a huge one-off staging buffer
+    (void)hipFree(t->dbuf);
+    t->dbuf = nullptr;
+    t->dcap = 0;
+  }
+  c->scalar->release(t);
+  return r;
 }
 
 // ---- host-buffer batch pipeline ----------------------------------------------
 
-constexpr uint64_t kStageBytes = 256ull << 20; // device staging per pipeline slot
-constexpr uint64_t kStageMaxBodies = 1ull << 20;
-
-struct HostSlot {
-  hipStream_t stream = nullptr;
-  uint8_t *dbuf = nullptr;   // device copy of the group's span
-  uint64_t *doff = nullptr;  // rebased offsets
-  uint32_t *dlen = nullptr;
-  uint32_t *dout = nullptr;
-  uint64_t *hoff = nullptr;  // pinned staging for metadata
-  uint32_t *hlen = nullptr;
-  uint32_t *hout = nullptr;
-  uint64_t first = 0, count = 0; // bodies of the group in flight
-  bool busy = false;
-};
-
-struct HostPipeline {
-  int device = -1;
-  HostSlot slot[2];
-  bool ok = false;
-};
-thread_local HostPipeline t_pipe;
-
-int pipe_init(HostPipeline &p, int dev) {
-  if (p.device == dev && p.ok) return RPCCRC_OK;
-  p.device = dev;
-  p.ok = false;
+int pipe_init(HostPipeline &p) {
+  if (p.ok) return RPCCRC_OK;
   for (HostSlot &s : p.slot) {
-    RPCCRC_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    RPCCRC_TRY(hipMalloc(&s.dbuf, kStageBytes));
-    RPCCRC_TRY(hipMalloc(&s.doff, kStageMaxBodies * 8));
-    RPCCRC_TRY(hipMalloc(&s.dlen, kStageMaxBodies * 4));
-    RPCCRC_TRY(hipMalloc(&s.dout, kStageMaxBodies * 4));
-    RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.hoff), kStageMaxBodies * 8, hipHostMallocDefault));
-    RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.hlen), kStageMaxBodies * 4, hipHostMallocDefault));
-    RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.hout), kStageMaxBodies * 4, hipHostMallocDefault));
+    if (!s.stream) RPCCRC_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    if (!s.dbuf) RPCCRC_TRY(hipMalloc(&s.dbuf, kStageBytes));
+    if (!s.doff) RPCCRC_TRY(hipMalloc(&s.doff, kStageMaxBodies * 8));
+    if (!s.dlen) RPCCRC_TRY(hipMalloc(&s.dlen, kStageMaxBodies * 4));
+    if (!s.dout) RPCCRC_TRY(hipMalloc(&s.dout, kStageMaxBodies * 4));
+    if (!s.hoff) RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.hoff), kStageMaxBodies * 8, hipHostMallocDefault));
+    if (!s.hlen) RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.hlen), kStageMaxBodies * 4, hipHostMallocDefault));
+    if (!s.hout) RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.hout), kStageMaxBodies * 4, hipHostMallocDefault));
   }
   p.ok = true;
   return RPCCRC_OK;
@@ -552,19 +648,16 @@ int pipe_init(HostPipeline &p, int dev) {
 
 int slot_drain(HostSlot &s, uint32_t *out) {
   if (!s.busy) return RPCCRC_OK;
+  s.busy = false;
   RPCCRC_TRY(hipStreamSynchronize(s.stream));
   memcpy(out + s.first, s.hout, s.count * 4);
-  s.busy = false;
   return RPCCRC_OK;
 }
 
-int host_batch(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-               uint32_t *out) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  int rc = pipe_init(t_pipe, dev);
+int host_batch_run(const DeviceCtx &c, HostPipeline &p, const uint8_t *base, const uint64_t *offsets,
+                   const uint32_t *lengths, uint64_t n, uint32_t *out) {
+  int rc = pipe_init(p);
   if (rc) return rc;
-  HostPipeline &p = t_pipe;
   uint64_t i = 0;
   int which = 0;
   while (i < n) {
@@ -573,14 +666,14 @@ int host_batch(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets,
       for (HostSlot &s : p.slot)
         if ((rc = slot_drain(s, out))) return rc;
       HostSlot &s = p.slot[0];
-      uint8_t *dtmp = nullptr;
       const uint64_t L = lengths[i];
-      RPCCRC_TRY(hipMallocAsync(reinterpret_cast<void **>(&dtmp), L, s.stream));
-      RPCCRC_TRY(hipMemcpyAsync(dtmp, base + offsets[i], L, hipMemcpyHostToDevice, s.stream));
-      const uint64_t zero = 0;
-      rc = device_large(c, dtmp, &zero, &L, 1, s.dout, 0, s.stream);
-      (void)hipFreeAsync(dtmp, s.stream);
-      if (rc) return rc;
+      {
+        Lease tmp;
+        if ((rc = tmp.get(c.ws, L, s.stream))) return rc;
+        RPCCRC_TRY(hipMemcpyAsync(tmp.ptr(), base + offsets[i], L, hipMemcpyHostToDevice, s.stream));
+        const uint64_t zero = 0;
+        if ((rc = device_large(c, tmp.ptr(), &zero, &L, 1, s.dout, 0, s.stream))) return rc;
+      }
       RPCCRC_TRY(hipMemcpyAsync(s.hout, s.dout, 4, hipMemcpyDeviceToHost, s.stream));
       s.first = i;
       s.count = 1;
@@ -611,7 +704,7 @@ int host_batch(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets,
     if (hi > lo) RPCCRC_TRY(hipMemcpyAsync(s.dbuf, base + lo, hi - lo, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.doff, s.hoff, cnt * 8, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.dlen, s.hlen, cnt * 4, hipMemcpyHostToDevice, s.stream));
-    rc = ragged(c, s.dbuf, s.doff, s.dlen, cnt, kModeFinal, s.dout, s.stream);
+    rc = ragged(c, s.dbuf, s.doff, s.dlen, cnt, kModeFinal, s.dout, s.stream, false, true);
     if (rc) return rc;
     RPCCRC_TRY(hipMemcpyAsync(s.hout, s.dout, cnt * 4, hipMemcpyDeviceToHost, s.stream));
     s.first = i;
@@ -623,6 +716,28 @@ int host_batch(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets,
     if ((rc = slot_drain(s, out))) return rc;
   return RPCCRC_OK;
 }
+
+int host_batch(DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+               uint32_t *out) {
+  HostPipeline *p = c.pipes->acquire();
+  const int rc = host_batch_run(c, *p, base, offsets, lengths, n, out);
+  if (rc) // leave the pipeline idle for its next borrower
+    for (HostSlot &s : p->slot)
+      if (s.busy) {
+        (void)hipStreamSynchronize(s.stream);
+        s.busy = false;
+      }
+  c.pipes->release(p);
+  return rc;
+}
+
+bool frames_flags_ok(int flags) {
+  const int role = flags & (RPC_FRAMES_SERVER | RPC_FRAMES_CLIENT);
+  return (flags & ~(RPC_FRAMES_SERVER | RPC_FRAMES_CLIENT | RPC_FRAMES_LIFT_CAP)) == 0 &&
+         (role == RPC_FRAMES_SERVER || role == RPC_FRAMES_CLIENT);
+}
+
+constexpr size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 } // namespace
 } // namespace rpccrc
@@ -678,7 +793,7 @@ int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, con
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) return rc;
-  return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream));
+  return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream), false, true);
 }
 
 int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_len, uint64_t stride, uint32_t *d_out,
@@ -706,46 +821,52 @@ int rpc_crc32_device_large(const uint8_t *d_base, const uint64_t *h_offsets, con
   return device_large(*c, d_base, h_offsets, h_lengths, n, d_out, chunk_bytes, static_cast<hipStream_t>(stream));
 }
 
-int rpc_frames_verify_device(const uint8_t *d_stream, const uint64_t *d_frame_offsets, uint64_t n, uint8_t *d_ok,
-                             uint32_t *d_crc, void *stream) {
+int rpc_frames_verify_device(const uint8_t *d_stream, uint64_t stream_bytes, const uint64_t *d_frame_offsets,
+                             uint64_t n, int flags, uint8_t *d_verdict, uint32_t *d_crc, void *stream) {
+  if (!frames_flags_ok(flags)) return RPCCRC_EINVAL;
   if (n == 0) return RPCCRC_OK;
-  if (!d_stream || !d_frame_offsets || !d_ok) return RPCCRC_EINVAL;
+  if (!d_stream || !d_frame_offsets || !d_verdict || n >= 0xFFFFFFFFull) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint8_t *ws = nullptr;
-  const size_t ws_bytes = n * (8 + 4 + 4 + 4);
-  RPCCRC_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), ws_bytes, s));
+  Lease wsl;
+  const size_t ws_bytes = align256(n * 8) + 3 * align256(n * 4) + align256(n);
+  if ((rc = wsl.get(c->ws, ws_bytes, s))) return rc;
+  uint8_t *ws = wsl.ptr();
   uint64_t *boff = reinterpret_cast<uint64_t *>(ws);
-  uint32_t *blen = reinterpret_cast<uint32_t *>(boff + n);
-  uint32_t *bexp = blen + n;
-  uint32_t *bcrc = d_crc ? d_crc : bexp + n;
-  rc = map_hip(launch_frames_parse(d_stream, d_frame_offsets, n, boff, blen, bexp, s));
-  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true);
-  if (rc == RPCCRC_OK) rc = map_hip(launch_frames_compare(bcrc, bexp, n, d_ok, s));
-  (void)hipFreeAsync(ws, s);
-  return rc;
+  uint32_t *blen = reinterpret_cast<uint32_t *>(ws + align256(n * 8));
+  uint32_t *bexp = reinterpret_cast<uint32_t *>(ws + align256(n * 8) + align256(n * 4));
+  uint32_t *bcrc = d_crc ? d_crc : reinterpret_cast<uint32_t *>(ws + align256(n * 8) + 2 * align256(n * 4));
+  uint8_t *pre = ws + align256(n * 8) + 3 * align256(n * 4);
+  RPCCRC_TRY(launch_frames_parse(d_stream, stream_bytes, d_frame_offsets, n, flags, boff, blen, bexp, pre, s));
+  const bool lift = (flags & RPC_FRAMES_LIFT_CAP) != 0;
+  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift))) return rc;
+  return map_hip(launch_frames_compare(bcrc, bexp, pre, n, d_verdict, s));
 }
 
-int rpc_frames_stamp_device(uint8_t *d_stream, const uint64_t *d_frame_offsets, const uint32_t *d_body_lens,
-                            uint64_t n, uint16_t version, uint16_t type, void *stream) {
+int rpc_frames_stamp_device(uint8_t *d_stream, uint64_t stream_bytes, const uint64_t *d_frame_offsets,
+                            const uint32_t *d_body_lens, uint64_t n, uint16_t version, uint16_t type, int flags,
+                            uint8_t *d_verdict, void *stream) {
+  if ((flags & ~(RPC_FRAMES_SERVER | RPC_FRAMES_CLIENT | RPC_FRAMES_LIFT_CAP)) != 0) return RPCCRC_EINVAL;
   if (n == 0) return RPCCRC_OK;
-  if (!d_stream || !d_frame_offsets || !d_body_lens) return RPCCRC_EINVAL;
+  if (!d_stream || !d_frame_offsets || !d_body_lens || n >= 0xFFFFFFFFull) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint8_t *ws = nullptr;
-  RPCCRC_TRY(hipMallocAsync(reinterpret_cast<void **>(&ws), n * (8 + 4), s));
+  Lease wsl;
+  const size_t ws_bytes = align256(n * 8) + 2 * align256(n * 4) + align256(n);
+  if ((rc = wsl.get(c->ws, ws_bytes, s))) return rc;
+  uint8_t *ws = wsl.ptr();
   uint64_t *boff = reinterpret_cast<uint64_t *>(ws);
-  uint32_t *bcrc = reinterpret_cast<uint32_t *>(boff + n);
-  rc = map_hip(launch_frames_body_offsets(d_frame_offsets, n, boff, s));
-  if (rc == RPCCRC_OK) rc = ragged(*c, d_stream, boff, d_body_lens, n, kModeFinal, bcrc, s, true);
-  if (rc == RPCCRC_OK)
-    rc = map_hip(launch_frames_stamp(d_stream, d_frame_offsets, d_body_lens, bcrc, n, version, type, s));
-  (void)hipFreeAsync(ws, s);
-  return rc;
+  uint32_t *blen = reinterpret_cast<uint32_t *>(ws + align256(n * 8));
+  uint32_t *bcrc = reinterpret_cast<uint32_t *>(ws + align256(n * 8) + align256(n * 4));
+  uint8_t *pre = d_verdict ? d_verdict : ws + align256(n * 8) + 2 * align256(n * 4);
+  RPCCRC_TRY(launch_frames_stamp_prep(stream_bytes, d_frame_offsets, d_body_lens, n, flags, boff, blen, pre, s));
+  const bool lift = (flags & RPC_FRAMES_LIFT_CAP) != 0;
+  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift))) return rc;
+  return map_hip(launch_frames_stamp(d_stream, d_frame_offsets, d_body_lens, bcrc, pre, n, version, type, s));
 }
 
 uint32_t rpc_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) { return crc32_combine(crc1, crc2, len2); }
@@ -767,8 +888,8 @@ int rpc_crc32_stream_read_device(const void *d_src, uint64_t nbytes, int pattern
 
 int rpc_crc32_set_options(int nontemporal, int max_blocks) {
   if (max_blocks < 0) return RPCCRC_EINVAL;
-  g_nontemporal = nontemporal ? 1 : 0;
-  g_max_blocks = max_blocks;
+  g_nontemporal.store(nontemporal ? 1 : 0);
+  g_max_blocks.store(max_blocks);
   return RPCCRC_OK;
 }
 
@@ -776,7 +897,7 @@ int rpc_crc32_set_ragged_path(int path) {
   if (path != RPCCRC_RAGGED_AUTO && path != RPCCRC_RAGGED_ROWS && path != RPCCRC_RAGGED_PACKED &&
       path != RPCCRC_RAGGED_SPLIT)
     return RPCCRC_EINVAL;
-  g_ragged_path = path;
+  g_ragged_path.store(path);
   return RPCCRC_OK;
 }
 

@@ -6,8 +6,9 @@
 // loop land many frames -- from any number of connections -- directly in
 // pinned host SEGMENTS (rpc_rx_ring_reserve hands out the destination for
 // recv()), and verifies a whole segment with one H2D copy, one
-// rpc_frames_verify_device launch (header parse + packed CRC kernel + compare)
-// and one D2H copy of the verdicts, while the next segment fills.  Results come
+// rpc_frames_verify_device launch (header parse with the reference's type / cap
+// rules, CRC kernels, compare) and one D2H copy of the verdicts, while the next
+// segment fills.  Results come
 // back in arrival order with the caller's tag (e.g. the connection fd), so the
 // dispatch step stays as it is.
 //
@@ -47,11 +48,11 @@ enum SegState { kFree, kFilling, kInflight };
 struct Segment {
   uint8_t *h_buf = nullptr;  // pinned frames, back to back
   uint64_t *h_off = nullptr; // pinned frame offsets
-  uint8_t *h_ok = nullptr;   // pinned verdicts (D2H)
+  uint8_t *h_verdict = nullptr; // pinned verdicts (D2H)
   uint32_t *h_crc = nullptr; // pinned body CRCs (D2H)
   uint8_t *d_buf = nullptr;
   uint64_t *d_off = nullptr;
-  uint8_t *d_ok = nullptr;
+  uint8_t *d_verdict = nullptr;
   uint32_t *d_crc = nullptr;
   std::vector<uint64_t> tags;
   size_t used = 0, nframes = 0;
@@ -77,6 +78,7 @@ struct DeviceGuard {
 
 struct rpc_rx_ring {
   int device = -1;
+  int flags = 0; // RPC_FRAMES_* (role, LIFT_CAP)
   hipStream_t stream = nullptr;
   size_t seg_bytes = 0, max_frames = 0;
   std::vector<Segment> seg;
@@ -97,11 +99,11 @@ void free_ring(rpc_rx_ring *r) {
   for (Segment &s : r->seg) {
     if (s.h_buf) (void)hipHostFree(s.h_buf);
     if (s.h_off) (void)hipHostFree(s.h_off);
-    if (s.h_ok) (void)hipHostFree(s.h_ok);
+    if (s.h_verdict) (void)hipHostFree(s.h_verdict);
     if (s.h_crc) (void)hipHostFree(s.h_crc);
     if (s.d_buf) (void)hipFree(s.d_buf);
     if (s.d_off) (void)hipFree(s.d_off);
-    if (s.d_ok) (void)hipFree(s.d_ok);
+    if (s.d_verdict) (void)hipFree(s.d_verdict);
     if (s.d_crc) (void)hipFree(s.d_crc);
     if (s.done) (void)hipEventDestroy(s.done);
   }
@@ -117,9 +119,10 @@ int submit_fill(rpc_rx_ring *r) {
   hipError_t e = hipMemcpyAsync(s.d_buf, s.h_buf, s.used, hipMemcpyHostToDevice, r->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, s.nframes * 8, hipMemcpyHostToDevice, r->stream);
   if (e != hipSuccess) return map_hip(e);
-  const int rc = rpc_frames_verify_device(s.d_buf, s.d_off, s.nframes, s.d_ok, s.d_crc, r->stream);
+  const int rc =
+      rpc_frames_verify_device(s.d_buf, s.used, s.d_off, s.nframes, r->flags, s.d_verdict, s.d_crc, r->stream);
   if (rc != RPCCRC_OK) return rc;
-  e = hipMemcpyAsync(s.h_ok, s.d_ok, s.nframes, hipMemcpyDeviceToHost, r->stream);
+  e = hipMemcpyAsync(s.h_verdict, s.d_verdict, s.nframes, hipMemcpyDeviceToHost, r->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(s.h_crc, s.d_crc, s.nframes * 4, hipMemcpyDeviceToHost, r->stream);
   if (e == hipSuccess) e = hipEventRecord(s.done, r->stream);
   if (e != hipSuccess) return map_hip(e);
@@ -132,16 +135,21 @@ int submit_fill(rpc_rx_ring *r) {
 
 extern "C" {
 
-int rpc_rx_ring_create(rpc_rx_ring_t **ring, size_t segment_bytes, size_t max_frames, int nsegments) {
+int rpc_rx_ring_create(rpc_rx_ring_t **ring, size_t segment_bytes, size_t max_frames, int nsegments, int flags) {
   if (!ring) return RPCCRC_EINVAL;
   *ring = nullptr;
   if (segment_bytes < kHdr || max_frames == 0 || nsegments < 2 || nsegments > 64) return RPCCRC_EINVAL;
+  const int role = flags & (RPC_FRAMES_SERVER | RPC_FRAMES_CLIENT);
+  if ((flags & ~(RPC_FRAMES_SERVER | RPC_FRAMES_CLIENT | RPC_FRAMES_LIFT_CAP)) != 0 ||
+      (role != RPC_FRAMES_SERVER && role != RPC_FRAMES_CLIENT))
+    return RPCCRC_EINVAL;
   int dev = -1, count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || hipGetDevice(&dev) != hipSuccess)
     return RPCCRC_ENODEV;
   rpc_rx_ring *r = new (std::nothrow) rpc_rx_ring;
   if (!r) return RPCCRC_ENOMEM;
   r->device = dev;
+  r->flags = flags;
   r->seg_bytes = segment_bytes;
   r->max_frames = max_frames;
   r->seg.resize((size_t)nsegments);
@@ -149,11 +157,11 @@ int rpc_rx_ring_create(rpc_rx_ring_t **ring, size_t segment_bytes, size_t max_fr
   for (Segment &s : r->seg) {
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_buf), segment_bytes, hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_off), max_frames * 8, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_ok), max_frames, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_verdict), max_frames, hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_crc), max_frames * 4, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_buf), segment_bytes);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_off), max_frames * 8);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_ok), max_frames);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_verdict), max_frames);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s.d_crc), max_frames * 4);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e == hipSuccess) s.tags.reserve(max_frames);
@@ -199,9 +207,17 @@ int rpc_rx_ring_commit(rpc_rx_ring_t *r, uint64_t tag) {
   const size_t len = r->reserved_len;
   r->reserved = nullptr;
   r->reserved_len = 0;
-  // The kernel reads body_len bytes after the header: it must be the frame the
-  // caller landed (rpc.h:6; the reference rejects bad lengths before its recv).
-  if ((uint64_t)be32(h + 4) + kHdr != len) return RPCCRC_EINVAL;
+  // The landed length must be what the reference reads for this header: the
+  // header alone for a control frame (rpc_server_main.c:172-187 PING at the
+  // server, rpc_async.c:303-309 PONG at the client) or a data frame over the
+  // cap (rpc_server_main.c:189-195, rpc_async.c:312: dropped before the body),
+  // else the header plus body_len bytes (rpc.h:6).
+  const uint64_t bl = be32(h + 4);
+  const uint16_t type = be16(h + 2);
+  const bool control = (type == RPC_FRAME_TYPE_PING && (r->flags & RPC_FRAMES_SERVER)) ||
+                       (type == RPC_FRAME_TYPE_PONG && (r->flags & RPC_FRAMES_CLIENT));
+  const bool over_cap = bl > RPC_MAX_BODY_LEN && !(r->flags & RPC_FRAMES_LIFT_CAP);
+  if (len != bl + kHdr && !(len == kHdr && (control || over_cap))) return RPCCRC_EINVAL;
   s.h_off[s.nframes] = s.used;
   s.tags.push_back(tag);
   s.used += len;
@@ -253,12 +269,13 @@ int64_t rpc_rx_ring_poll(rpc_rx_ring_t *r, rpc_rx_frame_t *out, size_t max_frame
     rpc_rx_frame_t &o = out[i];
     o.tag = h.tags[k];
     o.frame = f;
-    o.body_len = be32(f + 4);
+    o.body_len = be32(f + 4); // the header field (a control / over-cap frame landed no body)
     o.version = be16(f);
     o.type = be16(f + 2);
     o.header_crc = be32(f + 8);
     o.crc = h.h_crc[k];
-    o.ok = h.h_ok[k];
+    o.verdict = h.h_verdict[k];
+    o.ok = (o.verdict == RPC_FRAME_OK || o.verdict == RPC_FRAME_CONTROL) ? 1 : 0;
   }
   r->head_pos += n;
   if (r->head_pos == h.nframes) r->release_head = true;

@@ -17,10 +17,16 @@ EAGAIN = -11
 
 
 class RxRing:
-    def __init__(self, segment_bytes: int = 64 << 20, max_frames: int = 1 << 16, nsegments: int = 3):
+    def __init__(self, segment_bytes: int = 64 << 20, max_frames: int = 1 << 16, nsegments: int = 3,
+                 role: str = "server", lift_cap: bool = False):
         self._h = None
+        flags = {"server": 0x1, "client": 0x2}.get(role)
+        if flags is None:
+            raise ValueError("role must be 'server' or 'client'")
+        flags |= 0x4 if lift_cap else 0
         h = ctypes.c_void_p()
-        check(_lib.rpc_rx_ring_create(ctypes.byref(h), segment_bytes, max_frames, nsegments), "rpc_rx_ring_create")
+        check(_lib.rpc_rx_ring_create(ctypes.byref(h), segment_bytes, max_frames, nsegments, flags),
+              "rpc_rx_ring_create")
         self._h = h
         self._buf = (_lib.RxFrame * max_frames)()
         self.max_frames = max_frames
@@ -59,12 +65,15 @@ class RxRing:
     def submit(self):
         check(_lib.rpc_rx_ring_submit(self._h), "rpc_rx_ring_submit")
 
-    def poll(self, wait: bool = True) -> List[Tuple[int, int, int, int, bytes]]:
-        """[(tag, ok, crc, header_crc, body)] of the oldest submitted segment."""
+    def poll(self, wait: bool = True) -> List[Tuple[int, int, int, int, bytes, int]]:
+        """[(tag, ok, crc, header_crc, body, verdict)] of the oldest submitted segment.
+        ``body`` is empty for frames whose body the reference does not read
+        (control and over-cap frames land as the 12-byte header alone)."""
         n = check(_lib.rpc_rx_ring_poll(self._h, self._buf, self.max_frames, int(wait)), "rpc_rx_ring_poll")
         res = []
         for i in range(n):
             f = self._buf[i]
-            body = ctypes.string_at(f.frame + 12, f.body_len) if f.body_len else b""
-            res.append((int(f.tag), int(f.ok), int(f.crc), int(f.header_crc), body))
+            has_body = f.verdict in (0, 1) and f.body_len  # FRAME_BAD_CRC / FRAME_OK
+            body = ctypes.string_at(f.frame + 12, f.body_len) if has_body else b""
+            res.append((int(f.tag), int(f.ok), int(f.crc), int(f.header_crc), body, int(f.verdict)))
         return res

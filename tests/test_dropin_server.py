@@ -1,15 +1,27 @@
-"""Drop-in proof (test plan item 4): the reference's own `server`
-(built by `make -C oracle dropin` from /root/reference/server sources, with
-crc.c REPLACED by librpccrc.so, nothing else changed) answers framed JSON-RPC
-requests over loopback.  Its verify (rpc_server_main.c:227) and stamp
-(rpc_server_main.c:249) calls now run on the GPU through rpc_crc32 /
-rpc_crc32_verify.  Frames and CRCs are checked against the captured golden
-frames and the oracle."""
+"""Drop-in proof (test plan item 4), both halves of the reference.
+
+* Server: the reference's own `server` (built by `make -C oracle dropin` from
+  /root/reference/server sources, with crc.c REPLACED by librpccrc.so, nothing
+  else changed) answers framed JSON-RPC requests over loopback.  Its verify
+  (rpc_server_main.c:227) and stamp (rpc_server_main.c:249) run on the GPU.
+* Client: the reference's client library (rpc_async.c, conn_pool.c, pending.c,
+  epoll_api.c, rpc_codec.c, gen/rpc_client_gen.c) linked the same way, driven by
+  tests/dropin/client_driver.c with 10 user threads (rpc_client_main.c:17):
+  stamp at rpc_async.c:525 and receive-thread verify at rpc_async.c:219 on the
+  GPU; a corrupted response surfaces RPC_CRC_ERR (rpc_types.h:27).
+
+Frames and CRCs are checked against the captured golden frames and the oracle,
+and the batched frames verdicts (rpc_frames_verify_device) against what the
+reference server does with the same frames."""
+import json
 import os
 import socket
 import struct
 import subprocess
+import threading
 import time
+
+import numpy as np
 
 import pytest
 
@@ -19,6 +31,7 @@ pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SERVER = os.path.join(REPO, "oracle", "_ref", "server_rpccrc")
+CLIENT = os.path.join(REPO, "oracle", "_ref", "client_rpccrc")
 PORT = 8888  # hard-coded in the reference (rpc_server_main.c:65)
 
 
@@ -102,3 +115,122 @@ def test_ping_pong(server):
     s.sendall(struct.pack(">HHII", 1, 1, 0, 0))
     assert recv_exact(s, 12) == struct.pack(">HHII", 1, 2, 0, 0)
     s.close()
+
+
+def test_ping_with_crc_and_body_len_gets_pong(server):
+    """rpc_server_main.c:172-187 answers PING from the header alone: its crc32 and
+    body_len fields are never looked at (the batched verdict is FRAME_CONTROL)."""
+    s = socket.create_connection(("127.0.0.1", PORT), timeout=30)
+    s.sendall(struct.pack(">HHII", 3, 1, 777, 0xDEADBEEF))
+    assert recv_exact(s, 12) == struct.pack(">HHII", 3, 2, 0, 0)
+    s.close()
+
+
+def _server_outcome(raw: bytes) -> str:
+    """What the reference server does with one frame on a fresh connection."""
+    s = socket.create_connection(("127.0.0.1", PORT), timeout=30)
+    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    s.sendall(raw)
+    hdr = recv_exact(s, 12)
+    s.close()
+    if len(hdr) < 12:
+        return "closed"
+    return "pong" if struct.unpack(">HHII", hdr)[1] == 2 else "reply"
+
+
+def test_batched_verdicts_match_reference_server(server):
+    """The same frames through the reference server (one connection each) and through
+    rpc_frames_verify_device(role=server): PONG <-> FRAME_CONTROL, a reply <->
+    FRAME_OK, a closed connection <-> FRAME_BAD_CRC / FRAME_TOO_LARGE."""
+    torch = pytest.importorskip("torch")
+    import rpc_amd
+    good = b'{"jsonrpc":"2.0","method":"add_i32","params":{"a":1,"b":2},"id":3}'
+    frames = [
+        frame(good),
+        frame(good, crc=oracle.crc32(good) ^ 0x80000000),
+        struct.pack(">HHII", 1, 1, 0, 0),
+        struct.pack(">HHII", 1, 1, 64, 0x1234),            # PING with junk fields
+        struct.pack(">HHII", 1, 0, 1025, 0) + bytes(1025),  # over MAX_BODY_LEN
+        struct.pack(">HHII", 1, 0, 5000, 7),
+        frame(good, type_=9),                               # unknown type: data
+    ]
+    outcome = [_server_outcome(f) for f in frames]
+    offs, blob = [], b""
+    for f in frames:
+        offs.append(len(blob))
+        blob += f
+    v, _ = rpc_amd.frames_verify(torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).cuda(),
+                                 torch.tensor(offs, dtype=torch.int64).cuda(), role="server")
+    mapped = {rpc_amd.FRAME_CONTROL: "pong", rpc_amd.FRAME_OK: "reply", rpc_amd.FRAME_BAD_CRC: "closed",
+              rpc_amd.FRAME_TOO_LARGE: "closed"}
+    assert [mapped[x] for x in v.cpu().tolist()] == outcome
+    assert outcome == ["reply", "closed", "pong", "pong", "closed", "closed", "reply"]
+
+
+def _client(*args, timeout=120):
+    if not os.path.exists(CLIENT):
+        pytest.fail("oracle/_ref/client_rpccrc missing: build it with `make -C oracle dropin` (needs /root/reference)")
+    p = subprocess.run([CLIENT, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    return p.returncode, json.loads(p.stdout.strip().splitlines()[-1]), p.stderr
+
+
+def test_reference_client_10_threads(server):
+    """rpc_client_main.c's shape of work (10 user threads, THREAD_COUNT at :17) through
+    the reference client library on librpccrc: every request stamped on the GPU
+    (rpc_async.c:525), every response verified on the GPU (rpc_async.c:219), every
+    result correct."""
+    rc, res, err = _client("stress", PORT, 10, 5)
+    assert rc == 0 and res == {"success": 50, "failure": 0}, err[-2000:]
+
+
+def _bad_crc_server(port_holder, stop):
+    """A server that answers every DATA request with a response whose crc32 field is
+    wrong (and PING with PONG, as the reference server would)."""
+    ls = socket.socket()
+    ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    ls.bind(("127.0.0.1", 0))
+    ls.listen(64)
+    ls.settimeout(0.5)
+    port_holder.append(ls.getsockname()[1])
+
+    def serve(c):
+        try:
+            while not stop.is_set():
+                hdr = recv_exact(c, 12)
+                if len(hdr) < 12:
+                    return
+                ver, typ, blen, _ = struct.unpack(">HHII", hdr)
+                if typ == 1:
+                    c.sendall(struct.pack(">HHII", ver, 2, 0, 0))
+                    continue
+                req = json.loads(recv_exact(c, blen))
+                body = json.dumps({"jsonrpc": "2.0", "id": req["id"], "result": 3}, separators=(",", ":")).encode()
+                c.sendall(struct.pack(">HHII", ver, 0, len(body), oracle.crc32(body) ^ 0x00010000) + body)
+        except OSError:
+            return
+        finally:
+            c.close()
+
+    while not stop.is_set():
+        try:
+            c, _ = ls.accept()
+        except socket.timeout:
+            continue
+        threading.Thread(target=serve, args=(c,), daemon=True).start()
+    ls.close()
+
+
+def test_reference_client_flags_corrupted_response():
+    """rpc_async.c:219-222: a response whose body fails rpc_crc32_verify (on the GPU)
+    completes the call with RPC_CRC_ERR (= 5, rpc_types.h:27)."""
+    port, stop = [], threading.Event()
+    t = threading.Thread(target=_bad_crc_server, args=(port, stop), daemon=True)
+    t.start()
+    while not port:
+        time.sleep(0.05)
+    try:
+        rc, res, err = _client("raw", port[0], '{"jsonrpc":"2.0","method":"add_i32","params":{"a":1,"b":2},"id":1}')
+    finally:
+        stop.set()
+        t.join(timeout=5)
+    assert res == {"status": 5}, err[-2000:]

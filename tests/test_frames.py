@@ -1,0 +1,209 @@
+"""Frames on the GPU: batched verify / stamp of rpc.h wire
+frames, with the reference's receive-side decisions restated in
+``oracle.frame_verdict`` (type first -- PING at the server rpc_server_main.c:172-187,
+PONG at the client rpc_async.c:303-309 -- then the MAX_BODY_LEN cap
+rpc_server_main.c:189-195 / rpc_async.c:312, then rpc_crc32_verify) and the stream
+bound (no read outside the stream).  With the cap lifted (8f3) bodies of any size are
+verified, the large ones through the chunk route."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import rpc_amd  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+DEV = "cuda:0"
+HDR = 12
+
+
+def to_dev(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def header(body_len: int, crc: int, type_: int = 0, version: int = 1) -> bytes:
+    return (version.to_bytes(2, "big") + type_.to_bytes(2, "big") + (body_len & 0xFFFFFFFF).to_bytes(4, "big")
+            + (crc & 0xFFFFFFFF).to_bytes(4, "big"))
+
+
+def layout(frames, gap=0):
+    """Concatenate frames (bytes) with `gap` junk bytes after each; -> (stream, offsets)."""
+    offs, blob = [], bytearray()
+    for f in frames:
+        offs.append(len(blob))
+        blob += f + b"\xA5" * gap
+    return bytes(blob), np.array(offs, dtype=np.uint64)
+
+
+def verify(stream: bytes, offs, role="server", lift_cap=False, stream_bytes=None):
+    sdev = to_dev(np.frombuffer(stream, dtype=np.uint8).copy())
+    v, c = rpc_amd.frames_verify(sdev, to_dev(offs.view(np.int64)), role=role, lift_cap=lift_cap,
+                                 stream_bytes=stream_bytes)
+    return v.cpu().numpy().tolist(), u32(c).tolist()
+
+
+def expected(stream: bytes, offs, role="server", lift_cap=False):
+    r = [oracle.frame_verdict(stream, int(o), role, lift_cap) for o in offs]
+    return [x[0] for x in r], [x[1] for x in r]
+
+
+def test_frames_verify_and_stamp(golden):
+    rng = np.random.default_rng(2)
+    bodies = [f["body"].encode() for f in golden["frames"][:2]]
+    bodies += [rng.integers(32, 127, int(rng.integers(0, 1025)), dtype=np.uint8).tobytes() for _ in range(300)]
+    blob, offs = layout([bytes(HDR) + b for b in bodies], gap=1)
+    lens = np.array([len(b) for b in bodies], dtype=np.uint32)
+    dblob = to_dev(np.frombuffer(blob, dtype=np.uint8).copy())
+    sv = rpc_amd.frames_stamp(dblob, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32)), version=1,
+                              type_=rpc_amd.RPC_TYPE_DATA)
+    assert sv.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(bodies)
+    stamped = dblob.cpu().numpy().tobytes()
+    for i, (o, b) in enumerate(zip(offs, bodies)):
+        assert stamped[int(o):int(o) + HDR] == header(len(b), oracle.crc32(b)), i
+    # the captured request/response headers are reproduced byte for byte
+    assert stamped[:HDR].hex() == golden["frames"][0]["header_hex"]
+    assert stamped[int(offs[1]):int(offs[1]) + HDR].hex() == golden["frames"][1]["header_hex"]
+    # corrupt some bodies / CRC fields, then verify against the reference's decisions
+    arr = np.frombuffer(stamped, dtype=np.uint8).copy()
+    for i in range(4, len(bodies), 7):
+        if lens[i] > 0:
+            arr[int(offs[i]) + HDR + int(lens[i]) // 2] ^= 0x10
+        else:
+            arr[int(offs[i]) + 11] ^= 1
+    got = verify(arr.tobytes(), offs)
+    want = expected(arr.tobytes(), offs)
+    assert got == want
+    assert got[0].count(rpc_amd.FRAME_BAD_CRC) == len(range(4, len(bodies), 7))
+
+
+def test_captured_ping_pong(golden):
+    """The captured PING (client -> server) and PONG (server -> client) headers."""
+    ping, pong = (bytes.fromhex(f["header_hex"]) for f in golden["frames"][2:4])
+    stream, offs = layout([ping, pong])
+    v, _ = verify(stream, offs, role="server")
+    assert v == [rpc_amd.FRAME_CONTROL, rpc_amd.FRAME_OK]  # a server reads PONG as an (empty) data frame
+    v, _ = verify(stream, offs, role="client")
+    assert v == [rpc_amd.FRAME_OK, rpc_amd.FRAME_CONTROL]
+
+
+@pytest.mark.parametrize("role", ["server", "client"])
+@pytest.mark.parametrize("lift_cap", [False, True])
+def test_frames_type_rules(role, lift_cap):
+    """Heartbeats whose crc32 / body_len fields are not zero, unknown types, over-cap
+    lengths: every verdict and CRC equals the reference's decision."""
+    rng = np.random.default_rng(7 + lift_cap)
+    frames = []
+    for i in range(600):
+        kind = int(rng.integers(0, 8))
+        blen = int(rng.integers(0, 1500))
+        body = rng.integers(0, 256, blen, dtype=np.uint8).tobytes()
+        crc = oracle.crc32(body)
+        if kind == 0:  # PING with junk crc / body_len, landed as the header alone (server reads no body)
+            frames.append(header(blen, int(rng.integers(0, 2**32)), rpc_amd.RPC_TYPE_PING))
+        elif kind == 1:  # PONG likewise
+            frames.append(header(blen, int(rng.integers(0, 2**32)), rpc_amd.RPC_TYPE_PONG))
+        elif kind == 2:  # PING / PONG carrying a full, valid body
+            frames.append(header(blen, crc, int(rng.integers(1, 3))) + body)
+        elif kind == 3:  # unknown type: a data frame for both roles
+            frames.append(header(blen, crc, int(rng.integers(3, 65536))) + body)
+        elif kind == 4:  # corrupted crc field
+            frames.append(header(blen, crc ^ (1 << int(rng.integers(0, 32)))) + body)
+        else:
+            frames.append(header(blen, crc) + body)
+    stream, offs = layout(frames, gap=3)
+    assert verify(stream, offs, role, lift_cap) == expected(stream, offs, role, lift_cap)
+
+
+@pytest.mark.parametrize("lift_cap", [False, True])
+def test_frames_bounds_and_oversized_headers(lift_cap):
+    """a hostile header must not make the kernels read outside the stream.
+    body_len up to 0xFFFFFFFF, frames cut at the stream end, offsets past the end."""
+    good = b'{"jsonrpc":"2.0","id":1,"result":30}'
+    frames = [header(len(good), oracle.crc32(good)) + good,
+              header(0xFFFFFFF0, 0x12345678),           # oversized length, no body
+              header(2000, 0) + bytes(100),              # over cap, body cut short
+              header(len(good), oracle.crc32(good)) + good,
+              header(50, 0) + bytes(10)]                 # body runs past the stream end
+    stream, offs = layout(frames)
+    offs = np.concatenate([offs, np.array([len(stream) - 5, len(stream) + 100, 2**63], dtype=np.uint64)])
+    got = verify(stream, offs, lift_cap=lift_cap)
+    assert got == expected(stream, offs, lift_cap=lift_cap)
+    v = got[0]
+    assert v[0] == v[3] == rpc_amd.FRAME_OK
+    assert v[1] == (rpc_amd.FRAME_MALFORMED if lift_cap else rpc_amd.FRAME_TOO_LARGE)
+    assert v[4:] == [rpc_amd.FRAME_MALFORMED] * 4
+    # stream_bytes bounds the stream below the tensor's size
+    sub = int(offs[3])
+    v2, _ = verify(stream, offs[:4], lift_cap=lift_cap, stream_bytes=sub + HDR + len(good) - 1)
+    assert v2[3] == rpc_amd.FRAME_MALFORMED and v2[0] == rpc_amd.FRAME_OK
+
+
+def test_frames_stamp_cap_and_bounds():
+    """rpc_async.c:499-501: the client refuses to send a body over MAX_BODY_LEN, so
+    without LIFT_CAP it is not stamped; bodies past the stream end are not touched."""
+    lens = np.array([10, 1024, 1025, 5000, 7], dtype=np.uint32)
+    blob, offs = layout([bytes(HDR) + bytes(range(256)) * (int(L) // 256) + bytes(int(L) % 256) for L in lens])
+    offs = np.concatenate([offs, np.array([len(blob) - 3], dtype=np.uint64)])
+    lens = np.concatenate([lens, np.array([100], dtype=np.uint32)])
+    for lift in (False, True):
+        d = to_dev(np.frombuffer(blob, dtype=np.uint8).copy())
+        v = rpc_amd.frames_stamp(d, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32)), lift_cap=lift)
+        v = v.cpu().numpy().tolist()
+        TL = rpc_amd.FRAME_OK if lift else rpc_amd.FRAME_TOO_LARGE
+        assert v == [rpc_amd.FRAME_OK, rpc_amd.FRAME_OK, TL, TL, rpc_amd.FRAME_OK, rpc_amd.FRAME_MALFORMED]
+        out = d.cpu().numpy().tobytes()
+        for i in range(5):
+            o, L = int(offs[i]), int(lens[i])
+            want = header(L, oracle.crc32(out[o + HDR:o + HDR + L])) if v[i] == rpc_amd.FRAME_OK else bytes(HDR)
+            assert out[o:o + HDR] == want, (lift, i)
+        assert out[-3:] == blob[-3:]
+
+
+def test_frames_lifted_cap_large_bodies():
+    """frames with bodies from 1 B to 64 MiB (MAX_BODY_LEN lifted), stamped
+    then verified on the device; the bodies >= 256 KiB go through the chunk route."""
+    rng = np.random.default_rng(11)
+    lens = [1, 17, 1024, 1025, 4096, 65536, (256 << 10) - 1, 256 << 10, (256 << 10) + 1, (1 << 20) + 13,
+            (5 << 20) + 7, 3, (64 << 20) + 5, 0, (17 << 20) + 9, 300, 40000]
+    lens += rng.integers(0, 5000, 64).tolist()
+    total = sum(HDR + L + 1 for L in lens)
+    base = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0xF8A3E)
+    offs = np.cumsum([0] + [HDR + L + 1 for L in lens[:-1]]).astype(np.uint64)
+    dl = to_dev(np.array(lens, dtype=np.uint32).view(np.int32))
+    do = to_dev(offs.view(np.int64))
+    sv = rpc_amd.frames_stamp(base, do, dl, lift_cap=True, stream_bytes=total)
+    assert sv.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(lens)
+    host = base.cpu().numpy()
+    want_crc = [oracle.crc32(host[int(o) + HDR:int(o) + HDR + L]) for o, L in zip(offs, lens)]
+    for o, L, c in zip(offs, lens, want_crc):
+        assert host[int(o):int(o) + HDR].tobytes() == header(L, c)
+    v, c = rpc_amd.frames_verify(base, do, lift_cap=True, stream_bytes=total)
+    assert v.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(lens)
+    assert u32(c).tolist() == want_crc
+    # with the cap in force the same stream is TOO_LARGE above 1 KiB
+    v, _ = rpc_amd.frames_verify(base, do, lift_cap=False, stream_bytes=total)
+    assert v.cpu().numpy().tolist() == [rpc_amd.FRAME_OK if L <= 1024 else rpc_amd.FRAME_TOO_LARGE for L in lens]
+    # flip one byte inside the 64 MiB body and one inside a routed 1 MiB body
+    for k in (12, 9):
+        pos = int(offs[k]) + HDR + lens[k] // 3
+        base[pos] ^= 0x40
+    v, _ = rpc_amd.frames_verify(base, do, lift_cap=True, stream_bytes=total)
+    v = v.cpu().numpy().tolist()
+    assert [i for i, x in enumerate(v) if x != rpc_amd.FRAME_OK] == [9, 12]
+    assert v[9] == v[12] == rpc_amd.FRAME_BAD_CRC
+
+
+def test_frames_role_flags_rejected():
+    d = to_dev(np.zeros(64, dtype=np.uint8))
+    o = to_dev(np.zeros(1, dtype=np.int64))
+    v = torch.empty(1, dtype=torch.uint8, device=DEV)
+    for flags in (0, 3, 8, 1 | 8):
+        rc = rpc_amd._lib.rpc_frames_verify_device(d.data_ptr(), 64, o.data_ptr(), 1, flags, v.data_ptr(), None,
+                                                   rpc_amd._stream_handle(None))
+        assert rc == -22, flags

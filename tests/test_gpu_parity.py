@@ -363,58 +363,6 @@ def test_host_batch_spans_many_stages():
     assert got[n] == oracle.crc32(host[n * L:])
 
 
-# ---- frames (rpc.h wire format) ----------------------------------------------------
-
-def _build_frames(bodies, gap=0):
-    offs, blob = [], bytearray()
-    for b in bodies:
-        offs.append(len(blob))
-        blob += bytes(12) + b + bytes(gap)
-    return bytearray(blob), np.array(offs, dtype=np.uint64)
-
-
-def test_frames_verify_and_stamp(golden):
-    rng = np.random.default_rng(2)
-    bodies = [f["body"].encode() for f in golden["frames"]]
-    bodies += [rng.integers(32, 127, int(rng.integers(0, 1025)), dtype=np.uint8).tobytes() for _ in range(300)]
-    blob, offs = _build_frames(bodies, gap=1)
-    lens = np.array([len(b) for b in bodies], dtype=np.uint32)
-    dblob = to_dev(np.frombuffer(bytes(blob), dtype=np.uint8).copy())
-    rpc_amd.frames_stamp(dblob, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32)), version=1,
-                         type_=rpc_amd.RPC_TYPE_DATA)
-    stamped = dblob.cpu().numpy().tobytes()
-    for i, (o, b) in enumerate(zip(offs, bodies)):
-        hdr = stamped[int(o):int(o) + 12]
-        want = (1).to_bytes(2, "big") + (0).to_bytes(2, "big") + len(b).to_bytes(4, "big") + \
-            oracle.crc32(b).to_bytes(4, "big")
-        assert hdr == want, i
-    # the captured request/response headers are reproduced byte for byte
-    assert stamped[:12].hex() == golden["frames"][0]["header_hex"]
-    assert stamped[int(offs[1]):int(offs[1]) + 12].hex() == golden["frames"][1]["header_hex"]
-    # corrupt some bodies / CRC fields, then verify
-    arr = np.frombuffer(stamped, dtype=np.uint8).copy()
-    bad = set()
-    for i in range(4, len(bodies), 7):
-        if lens[i] > 0:
-            arr[int(offs[i]) + 12 + int(lens[i]) // 2] ^= 0x10
-        else:
-            arr[int(offs[i]) + 11] ^= 1
-        bad.add(i)
-    ok, crc = rpc_amd.frames_verify(to_dev(arr), to_dev(offs.view(np.int64)))
-    ok = ok.cpu().numpy()
-    for i in range(len(bodies)):
-        assert ok[i] == (0 if i in bad else 1), i
-    body_crc = [oracle.crc32(arr[int(o) + 12:int(o) + 12 + int(L)]) for o, L in zip(offs, lens)]
-    assert u32(crc).tolist() == body_crc
-
-
-def test_frames_ping_pong(golden):
-    hdrs = b"".join(bytes.fromhex(f["header_hex"]) for f in golden["frames"][2:])
-    ok, _ = rpc_amd.frames_verify(to_dev(np.frombuffer(hdrs, np.uint8).copy()),
-                                  to_dev(np.array([0, 12], dtype=np.int64)))
-    assert ok.cpu().tolist() == [1, 1]
-
-
 # ---- BASELINE.json full sizes: size-independent properties --------------------------
 
 def _sample_check(base_dev, n, L, stride, got, k=1500, seed=0):
@@ -509,3 +457,144 @@ def test_c4_large_bodies():
         for c in per[i * (L // sub) + 1:(i + 1) * (L // sub)]:
             acc = oracle.combine(acc, int(c), sub)
         assert got[i] == acc
+
+
+# ---- big bodies inside ragged batches: the device-side chunk route ----
+
+BIG = 256 << 10  # kBigMin
+
+
+@pytest.mark.parametrize("path", ["auto", "split"])
+@pytest.mark.parametrize("misalign", [0, 5])
+def test_device_batch_big_bodies_route(path, misalign):
+    """Bodies around and far above the 256 KiB route threshold, mixed with small and
+    empty ones, unordered: every CRC against the oracle."""
+    lens = [3, BIG - 1, BIG, BIG + 1, 0, (1 << 20) + 13, 17, (64 << 20) + 5, 1000, (9 << 20) - 16, 4096,
+            (2 << 20), 5000, BIG + 4097]
+    offs = (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]) + misalign).astype(np.uint64)
+    perm = np.random.default_rng(misalign).permutation(len(lens))
+    lens_p = np.array(lens, dtype=np.uint32)[perm]
+    offs_p = offs[perm]
+    base = torch.empty(int(offs[-1]) + lens[-1] + 16, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0xB16B0D1E + misalign)
+    rpc_amd.set_ragged_path(path)
+    try:
+        got = u32(rpc_amd.device_batch(base, to_dev(offs_p.view(np.int64)), to_dev(lens_p.view(np.int32))))
+    finally:
+        rpc_amd.set_ragged_path("auto")
+    host = base.cpu().numpy()
+    assert got.tolist() == oracle.crc32_batch(host, offs_p, lens_p).tolist()
+
+
+def test_device_batch_route_overflow_and_overlap():
+    """More big bodies than the route holds (16384): the extra ones keep one wave each;
+    overlapping bodies; the same buffer region listed many times."""
+    n_big = 16384 + 37
+    L = BIG + 48
+    region = torch.empty(4 << 20, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(region, 0x0FF10)
+    rng = np.random.default_rng(9)
+    offs = rng.integers(0, (4 << 20) - L, n_big).astype(np.uint64)
+    lens = np.full(n_big, L, dtype=np.uint32)
+    lens[::97] = rng.integers(0, 3000, lens[::97].size)  # small ones in between
+    got = u32(rpc_amd.device_batch(region, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    want = oracle.crc32_batch_mt(region.cpu().numpy(), offs, lens)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"{bad.size} mismatches, first {int(bad[0])}"
+
+
+def test_device_batch_route_chunk_growth():
+    """More than kBigMaxChunks x 16 KiB of routed bytes: the plan doubles the chunk.
+    Five 3.75 GiB bodies over one region (18.75 GiB routed); the CRC of the region is
+    known from the north-star-style check of checksums."""
+    L = (15 << 28)  # 3.75 GiB
+    region = torch.empty(L + 64, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(region, 0xC4C4)
+    offs = np.array([0, 16, 0, 64, 16], dtype=np.uint64)
+    lens = np.array([L, L, L - 16, L, L], dtype=np.uint32)
+    got = u32(rpc_amd.device_batch(region, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))))
+    # reference values: the large-body path (16 KiB chunks, host table) per distinct body
+    for o, ln, g in zip(offs, lens, got):
+        want = u32(rpc_amd.device_large(region, [int(o)], [int(ln)], chunk=4096 + 16))[0]
+        assert g == want, (int(o), int(ln))
+    # and one of them fully on the CPU
+    host = region[:L].cpu().numpy()
+    assert got[0] == oracle.crc32(host)
+
+
+def _hip_runtime():
+    """The HIP runtime torch loaded (the same copy librpccrc binds to)."""
+    import ctypes
+    for line in open("/proc/self/maps"):
+        if "libamdhip64" in line:
+            return ctypes.CDLL(line.split()[-1])
+    raise RuntimeError("libamdhip64 not loaded")
+
+
+class _RawStream:
+    """A hipStream_t of our own, so the test can really destroy one."""
+
+    def __init__(self, hip):
+        import ctypes
+        self.hip, h = hip, ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        self.cuda_stream = h.value
+
+    def destroy(self):
+        import ctypes
+        assert self.hip.hipStreamDestroy(ctypes.c_void_p(self.cuda_stream)) == 0
+
+
+def test_workspace_pool_stream_switches():
+    """cached workspaces across stream switches, growth while earlier work is
+    in flight, a destroyed stream, and the scalar path alternating with the batch path."""
+    hip = _hip_runtime()
+    n, L = 12, 9 << 20
+    base = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0x5EEDF00D)
+    host = base.cpu().numpy()
+    want = [oracle.crc32(host[i * L:(i + 1) * L]) for i in range(n)]
+    torch.cuda.synchronize()
+    s1, s2 = _RawStream(hip), _RawStream(hip)
+    outs = []
+    for stream, k, chunk in [(s1, 2, 0), (s2, 12, 4096), (s1, 6, 1024), (s2, 12, 256)]:
+        o = torch.empty(k, dtype=torch.int32, device=DEV)
+        rpc_amd.device_large(base, [i * L for i in range(k)], [L] * k, chunk=chunk, out=o, stream=stream)
+        outs.append((o, k))
+    s2.destroy()  # its last call may still be in flight; the pool must not care
+    s3 = _RawStream(hip)
+    o3 = torch.empty(n, dtype=torch.int32, device=DEV)
+    rpc_amd.device_large(base, [i * L for i in range(n)], [L] * n, chunk=2048, out=o3, stream=s3)
+    # ragged batches (split + route workspaces) on the same streams
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    lens = np.full(n, L, dtype=np.uint32)
+    o4 = torch.empty(n, dtype=torch.int32, device=DEV)
+    rpc_amd.device_batch(base, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32)), out=o4, stream=s1)
+    assert hip.hipDeviceSynchronize() == 0
+    for o, k in outs:
+        assert u32(o).tolist() == want[:k]
+    assert u32(o3).tolist() == want
+    assert u32(o4).tolist() == want
+    s1.destroy()
+    s3.destroy()
+    # drop-in rpc_crc32 (>= 8 MiB: chunked path) alternating with rpc_crc32_batch
+    for i in range(3):
+        assert rpc_amd.rpc_crc32(host[i * L:(i + 1) * L]) == want[i]
+        assert rpc_amd.crc32_batch(host, offs, lens).tolist() == want
+        assert rpc_amd.rpc_crc32(host[:100]) == oracle.crc32(host[:100])
+
+
+def test_c3_per_rank_shard_full_coverage():
+    """Config C3's per-GPU shard at full size: 8M x 4 KiB = 32 GiB on one GPU (rank 0's
+    seed), EVERY CRC against the oracle (threaded, 4 GiB at a time)."""
+    n, L = 1 << 23, 4096
+    x = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(x, 0x5EED0005)
+    got = u32(rpc_amd.device_uniform(x, n, L))
+    step = 1 << 20
+    for lo in range(0, n, step):
+        part = x[lo * L:(lo + step) * L].cpu().numpy()
+        want = oracle.crc32_uniform_mt(part, step, L)
+        bad = np.flatnonzero(got[lo:lo + step] != want)
+        assert bad.size == 0, f"{bad.size} mismatches, first body {lo + int(bad[0])}"
+        del part

@@ -39,6 +39,13 @@ def test_ring_rejects_bad_geometry():
         with pytest.raises(rpc_amd.RpcCrcError) as ei:
             rpc_amd.RxRing(*args)
         assert ei.value.code == -22
+    # exactly one role bit (server: PING is control, client: PONG), LIFT_CAP optional
+    import ctypes
+    for flags in (0, 3, 4, 8, 1 | 8):
+        h = ctypes.c_void_p()
+        assert rpc_amd._lib.rpc_rx_ring_create(ctypes.byref(h), 1 << 16, 64, 2, flags) == -22, flags
+    with pytest.raises(ValueError):
+        rpc_amd.RxRing(1 << 16, 64, 2, role="proxy")
 
 
 def _workload(n, seed):
@@ -83,6 +90,8 @@ def test_ring_verdicts_match_reference(seg_bytes, max_frames, nseg):
     assert [g[1] for g in got] == ok
     assert [g[2] for g in got] == crcs
     assert [g[4] for g in got] == [f[12:] for f in frames]
+    assert [g[5] for g in got] == [rpc_amd.FRAME_CONTROL if f[2:4] == b"\x00\x01" else
+                                   (rpc_amd.FRAME_OK if k else rpc_amd.FRAME_BAD_CRC) for f, k in zip(frames, ok)]
 
 
 @pytest.mark.gpu
@@ -131,3 +140,62 @@ def test_ring_partial_polls_and_idle():
             got += ring.poll(wait=True)
         assert ring.poll(wait=True) == []
     assert [g[1] for g in got] == ok
+
+
+def _hdr(body_len, crc, type_=rpc_amd.RPC_TYPE_DATA):
+    return (1).to_bytes(2, "big") + type_.to_bytes(2, "big") + body_len.to_bytes(4, "big") + crc.to_bytes(4, "big")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("role", ["server", "client"])
+def test_ring_control_and_over_cap_frames(role):
+    """The reference reads no body for a heartbeat (PING at the server,
+    rpc_server_main.c:172-187; PONG at the client, rpc_async.c:303-309) whatever its
+    crc32 / body_len fields hold, nor for a data frame over MAX_BODY_LEN
+    (rpc_server_main.c:189-195, rpc_async.c:312): such frames land as the 12-byte
+    header alone and get FRAME_CONTROL / FRAME_TOO_LARGE."""
+    ctl = rpc_amd.RPC_TYPE_PING if role == "server" else rpc_amd.RPC_TYPE_PONG
+    other = rpc_amd.RPC_TYPE_PONG if role == "server" else rpc_amd.RPC_TYPE_PING
+    body = b'{"jsonrpc":"2.0","id":7,"result":1}'
+    frames = [
+        (_hdr(500, 0xDEADBEEF, ctl), rpc_amd.FRAME_CONTROL, 1),
+        (_hdr(0, 0, ctl), rpc_amd.FRAME_CONTROL, 1),
+        (_hdr(2000, 0x1234), rpc_amd.FRAME_TOO_LARGE, 0),
+        (_hdr(1025, 0) + bytes(1025), rpc_amd.FRAME_TOO_LARGE, 0),  # landed whole: still over the cap
+        (frame(body), rpc_amd.FRAME_OK, 1),
+        (frame(body, type_=other), rpc_amd.FRAME_OK, 1),          # the other heartbeat type is data here
+        (frame(body, type_=other, crc=5), rpc_amd.FRAME_BAD_CRC, 0),
+        (frame(b"", type_=other), rpc_amd.FRAME_OK, 1),
+    ]
+    with rpc_amd.RxRing(1 << 16, 64, 2, role=role) as ring:
+        for i, (f, _, _) in enumerate(frames):
+            assert ring.push_into(f, i) == 0
+        # a data frame landed as a bare header while its body_len is within the cap is refused
+        with pytest.raises(rpc_amd.RpcCrcError):
+            ring.push(_hdr(100, 0), 99)
+        ring.submit()
+        got = ring.poll(wait=True)
+    assert [g[0] for g in got] == list(range(len(frames)))
+    assert [g[5] for g in got] == [v for _, v, _ in frames]
+    assert [g[1] for g in got] == [ok for _, _, ok in frames]
+    assert got[4][4] == body and got[0][4] == b"" and got[2][4] == b""
+
+
+@pytest.mark.gpu
+def test_ring_lifted_cap_large_frames():
+    """SURVEY 8f3 through the ring: bodies up to 6 MiB in 16 MiB segments, verified on
+    the GPU (the >= 256 KiB ones through the chunk route), one corrupted."""
+    rng = np.random.default_rng(5)
+    lens = [3000, 1 << 20, (6 << 20) + 5, 17, (256 << 10) + 1, 1024, 70000, (3 << 20) + 11]
+    bodies = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    frames = [frame(b) for b in bodies]
+    bad = bytearray(frames[2])
+    bad[12 + 4321] ^= 1
+    frames[2] = bytes(bad)
+    with rpc_amd.RxRing(16 << 20, 64, 2, lift_cap=True) as ring:
+        for i, f in enumerate(frames):
+            assert ring.push(f, i) == 0
+        ring.submit()
+        got = ring.poll(wait=True)
+    assert [g[5] for g in got] == [rpc_amd.FRAME_BAD_CRC if i == 2 else rpc_amd.FRAME_OK for i in range(len(lens))]
+    assert [g[2] for g in got] == [oracle.crc32(f[12:]) for f in frames]

@@ -68,7 +68,7 @@ int main(int argc, char **argv) {
   }
   rpc_rx_ring_t *ring = NULL;
   const size_t max_frames = seg / flen + 1;
-  rc = rpc_rx_ring_create(&ring, seg, max_frames, nseg);
+  rc = rpc_rx_ring_create(&ring, seg, max_frames, nseg, RPC_FRAMES_SERVER);
   if (rc) {
     fprintf(stderr, "rpc_rx_ring_create: %s\n", rpc_crc32_strerror(rc));
     return 1;
