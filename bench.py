@@ -33,6 +33,19 @@ sys.path.insert(0, REPO)
 torch = None
 rpc_amd = None
 
+
+def _load_gpu_modules():
+    """Import torch and rpc_amd (HIP runtime) on first use."""
+    global torch, rpc_amd
+    if torch is None:
+        import torch as _torch
+
+        torch = _torch
+    if rpc_amd is None:
+        import rpc_amd as _rpc_amd
+
+        rpc_amd = _rpc_amd
+
 METRIC = "GiB/s CRC32 over device-resident batched bodies; 1/2/4/8 MI355X"
 HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 GiB = float(1 << 30)
@@ -75,6 +88,7 @@ def parse():
 
 class Workload:
     def __init__(self, cfg: str, rank: int, device, chunk: int = 0):
+        _load_gpu_modules()
         desc, kind, n, L, seed = CONFIGS[cfg]
         self.name, self.desc, self.kind, self.n, self.L = cfg, desc, kind, n, L
         self.chunk = chunk
@@ -337,12 +351,7 @@ def main():
         print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus,
                           "master": os.environ.get("MASTER_ADDR")}), flush=True)
         return
-    global torch, rpc_amd
-    import torch as _torch
-
-    import rpc_amd as _rpc_amd
-
-    torch, rpc_amd = _torch, _rpc_amd
+    _load_gpu_modules()
     from rpc_amd.shard import barrier, max_over_ranks, sum_over_ranks
 
     if world != args.gpus:

@@ -91,6 +91,10 @@ struct CombineArgs {
   InlineBodies bodies;
 };
 
+// Most items one rows-kernel launch takes (it indexes them in 32 bits);
+// launch_rows splits larger host-counted batches.
+constexpr uint64_t kMaxLaunchItems = 1ull << 30;
+
 // QB = 1: rows of 4 KiB of one item (any length); QB = 4: four items per row,
 // each with len + ((-(end address)) & 15) <= 1024.
 hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream);

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include <rocprim/device/device_scan.hpp>
 
 #include "crc32_gf2.h"
@@ -175,6 +177,25 @@ static constexpr int kBlock = 1024;
 
 hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream) {
   if (a.n_items == 0) return hipSuccess;
+  // The kernel indexes items and tasks in 32 bits: launches of at most
+  // kMaxLaunchItems (a multiple of 4: QB = 4 groups never straddle launches).
+  if (a.n_items > kMaxLaunchItems) {
+    if (a.n_dev != nullptr || a.out_idx != nullptr || a.routed != nullptr) return hipErrorInvalidValue;
+    for (uint64_t s0 = 0; s0 < a.n_items; s0 += kMaxLaunchItems) {
+      ItemsArgs b = a;
+      b.n_items = std::min<uint64_t>(kMaxLaunchItems, a.n_items - s0);
+      if (b.offsets) {
+        b.offsets += s0;
+        b.lengths += s0;
+      } else {
+        b.base += s0 * a.stride;
+      }
+      b.out += s0;
+      const hipError_t e = launch_rows(b, QB, nt, max_blocks, stream);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   // One row per step (PAIR = 1), 16-wave (1024-thread) workgroups, one per CU.
   constexpr int kWaves = 16;
   const uint64_t per_wave = (QB == 4) ? 4 : 1;
@@ -393,7 +414,7 @@ hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes,
                               hipStream_t s) {
   const uint64_t n = proto.n_items;
   if (n == 0) return hipSuccess;
-  if (n >= 0xFFFFFFFFull || proto.offsets == nullptr || proto.lengths == nullptr) return hipErrorInvalidValue;
+  if (n > kMaxLaunchItems || proto.offsets == nullptr || proto.lengths == nullptr) return hipErrorInvalidValue;
   uint8_t *w = static_cast<uint8_t *>(ws);
   auto take = [&](size_t bytes) {
     uint8_t *r = w;
@@ -602,7 +623,7 @@ BigRoute big_route_carve(void *ws, uint64_t n) {
 
 hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, const BigRoute &r, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (n >= 0xFFFFFFFFull) return hipErrorInvalidValue;
+  if (n > kMaxLaunchItems) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(r.meta, 0, 32, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(big_classify_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lengths, n, r);

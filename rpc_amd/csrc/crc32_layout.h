@@ -21,8 +21,19 @@ constexpr uint32_t kLdsBytesV2 = 158736;     // rows-kernel image (155 KiB)
 constexpr uint32_t kMaxRow = 4096;           // 64 lanes x 64-byte segments
 constexpr uint32_t kTqEntries = kMaxRow + 1; // Tq[q] = A_q(0xFFFFFFFF), q=0..4096
 
+// Two independent slice-by-4 chains per lane (crc32_rows.h seg_crc2 /
+// merge_lo2): each lane's 64-B segment is CRC'd as two 32-B halves whose
+// dependent LDS round trips interleave; the ST1 copies of banks 16..31 then
+// carry the extra A_32 of the first half.  Off: measured slower (NS 640 vs 622 us,
+// C2 7200 vs 6890 us, one box, profiles/r02/r02d_two_chains_ab.txt) -- the kernel
+// is bound by board power (instructions per byte), not by the chain latency.
+#ifndef RPCCRC_TWO_CHAINS
+#define RPCCRC_TWO_CHAINS 0
+#endif
+constexpr bool kTwoChains = RPCCRC_TWO_CHAINS != 0;
+
 // ---- rows-kernel image (crc32_rows.h): main tables as above, then
-//   ST1 16 KiB  A_{64*(15-(c&15))}(nib << 4n), c = lane & 31, at
+//   ST1 16 KiB  A_{64*(15-(c&15)) + (kTwoChains ? 32*((c>>4)&1) : 0)}(nib << 4n), c = lane & 31, at
 //               ST1 + (n/2)*4096 + nib*256 + (n%2)*128 + c*4: one v_perm_b32 of
 //               the masked nibble vector forms the address (like MAIN), the
 //               n/2 part rides in the ds_read immediate offset

@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   // of quarter hi (crc32_rows.h).
   auto quarter_crcs = [&](u32x4 (&buf)[4]) -> uint32_t {
     transpose(buf);
-    return merge_lo(lds, seg_crc(lds, buf, lsel), lsel1);
+    return row_quarters(lds, buf, lsel, lsel1, (lane & 16u) != 0);
   };
 
   uint32_t W = 0; // register of the body continuing into the next row (uniform)

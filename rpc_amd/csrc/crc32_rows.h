@@ -140,7 +140,7 @@ __device__ __forceinline__ u32x4 ldb16(__amdgpu_buffer_rsrc_t rsrc, uint32_t off
 // is replaced by one past the descriptor's range (raw buffer range check).
 template <bool NT>
 __device__ __forceinline__ u32x4 ldb16_or_zero(__amdgpu_buffer_rsrc_t rsrc, int32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, off >= 0 ? off : (int)kOobOffset, 0, NT ? 2 : 0);
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)min((uint32_t)off, kOobOffset), 0, NT ? 2 : 0);
 }
 
 // Edge fix of one quarter of 16-B pieces (replaces a per-lane byte mask of
@@ -150,19 +150,24 @@ __device__ __forceinline__ u32x4 ldb16_or_zero(__amdgpu_buffer_rsrc_t rsrc, int3
 // body's first byte (window offset `front`, its front & 15 leading bytes are
 // foreign) and the window's last piece when it ends in the z pad (its last z
 // bytes).  `front` >= 1024 (or a multiple of 16) and z = 0 disable a fix.
+// x & (m | e) in one v_bitop3_b32 (truth table 0xE0): m is the scalar dword
+// mask, e is all-ones in every lane but the edge lane.
+__device__ __forceinline__ uint32_t and_or_keep(uint32_t x, uint32_t m, uint32_t e) {
+  return __builtin_amdgcn_bitop3_b32(x, m, e, 0xE0);
+}
 template <bool NATURAL = false>
 __device__ __forceinline__ void fix_quarter(u32x4 &x, uint32_t lane, uint32_t front, uint32_t z) {
   auto lane_of = [](uint32_t p) { return NATURAL ? p : lane_of_piece(p); };
   if ((front & 15u) != 0u && front < 1024u) {
-    const bool me = lane == lane_of(front >> 4);
+    const uint32_t e = (lane == lane_of(front >> 4)) ? 0u : 0xFFFFFFFFu;
     const uint32_t f = front & 15u;
 #pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) x[d] &= me ? keep_dword(f, 16u, d) : 0xFFFFFFFFu;
+    for (uint32_t d = 0; d < 4; ++d) x[d] = and_or_keep(x[d], keep_dword(f, 16u, d), e);
   }
   if (z != 0u) {
-    const bool me = lane == lane_of(63u);
+    const uint32_t e = (lane == lane_of(63u)) ? 0u : 0xFFFFFFFFu;
 #pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) x[d] &= me ? keep_dword(0u, 16u - z, d) : 0xFFFFFFFFu;
+    for (uint32_t d = 0; d < 4; ++d) x[d] = and_or_keep(x[d], keep_dword(0u, 16u - z, d), e);
   }
 }
 
@@ -213,6 +218,32 @@ __device__ __forceinline__ uint32_t seg_crc(const uint8_t *lds, const u32x4 (&p)
       x = slice4w(lds, x, p[k][d], lsel);
     }
   return slice4(lds, x, lsel);
+}
+
+// Two independent chains per lane (kTwoChains): a = crc0 of the segment's
+// first 32 bytes (slots 0, 1), b = crc0 of its last 32 bytes (slots 2, 3).
+// Their LDS round trips interleave, so a segment costs 8 dependent steps
+// instead of 16 (the chain is latency-bound: 4 waves per SIMD).
+struct Seg2 {
+  uint32_t a, b;
+};
+__device__ __forceinline__ Seg2 seg_crc2(const uint8_t *lds, const u32x4 (&p)[4], uint32_t lsel) {
+  uint32_t xa = p[0][0], xb = p[2][0];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (k == 0 && d == 0) continue;
+      xa = slice4w(lds, xa, p[k][d], lsel);
+      xb = slice4w(lds, xb, p[k + 2][d], lsel);
+    }
+  return Seg2{slice4(lds, xa, lsel), slice4(lds, xb, lsel)};
+}
+
+// The value of lane L ^ 16 (swap across lane bit 4), `upper` = lane & 16.
+__device__ __forceinline__ uint32_t swap_lanebit4(uint32_t v, bool upper) {
+  auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return upper ? a[0] : a[1];
 }
 
 // Workgroup copy of the kBytes LDS table image (1024 threads): all of a
@@ -332,6 +363,31 @@ __device__ __forceinline__ uint32_t merge_lo(const uint8_t *lds, uint32_t s, uin
   return s ^ dpp_ror8(s);
 }
 
+// Merge step 1 for two chains: the segment's crc0 is A_{S+32}(a) ^ A_S(b),
+// S = 64*(15-lo).  A lane reads ST1 only in its own bank (conflict-free), and
+// bank c holds shift S + 32*((c >> 4) & 1): lanes with lane bit 4 clear hold
+// S, their partners L ^ 16 (same lo) hold S + 32.  So each lane shifts its own
+// value of its bank's kind and its partner's value of the same kind, then
+// hands the partner's result back: two ST1 passes, two lane-bit-4 swaps.
+__device__ __forceinline__ uint32_t merge_lo2(const uint8_t *lds, Seg2 c, uint32_t lsel1, bool upper) {
+  const uint32_t own = upper ? c.a : c.b;
+  const uint32_t other = swap_lanebit4(upper ? c.b : c.a, upper);
+  const uint32_t t_own = st1_map(lds, own, lsel1);
+  const uint32_t t_other = st1_map(lds, other, lsel1);
+  uint32_t s = t_own ^ swap_lanebit4(t_other, upper);
+  s ^= dpp_xor1(s);
+  s ^= dpp_xor2(s);
+  s ^= dpp_ror4(s);
+  return s ^ dpp_ror8(s);
+}
+
+// Transposed row -> every lane of 16-lane row hi holds crc0 of quarter hi.
+__device__ __forceinline__ uint32_t row_quarters(const uint8_t *lds, const u32x4 (&p)[4], uint32_t lsel,
+                                                 uint32_t lsel1, bool upper) {
+  if constexpr (kTwoChains) return merge_lo2(lds, seg_crc2(lds, p, lsel), lsel1, upper);
+  else return merge_lo(lds, seg_crc(lds, p, lsel), lsel1);
+}
+
 // Merge step 2 for QB = 1 fused with the Horner step of the previous rows:
 // one ds_read per lane serves both the per-quarter ST2 shift A_{1024*(3-hi)}
 // of v_hi (lanes lo < 8, nibble lo) and RW(u) = A_4096(u) of the wave-uniform
@@ -413,11 +469,15 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   const uint32_t lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);  // MAIN tables
   const uint32_t lsel1 = lane4 | ((lane4 + 128u) << 8) | (2u << 16); // ST1
   const uint32_t hi = lane >> 4;                   // 16-lane row = quarter after the transpose
+  const bool upper = (lane & 16u) != 0;            // lane bit 4 (two-chain merge)
   // byte offset of this lane's piece in a quarter
   const uint32_t pofs = 16u * (((ABL & kRowsAblNaturalOrder) != 0) ? lane : piece_of_lane(lane));
   const DistLane dl = dist_lane(lane);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = (uint64_t)gridDim.x * 16u;
+  // Task / item indices are 32-bit (launch_rows keeps every launch below 2^30
+  // items): SALU has no 64-bit ordered compare, so 64-bit indices put every
+  // `task < n` test (and its operand copies) on the VALU.
+  const uint32_t nwaves = gridDim.x * 16u;
   // Tasks (QB = 1: items, QB = 4: groups of 4 items) are dealt round-robin in
   // groups of G (below): all waves stream one moving window of HBM (blocked
   // ranges put 4096 streams 1 MiB apart in lockstep: measured 6 % slower).
@@ -428,30 +488,30 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // XCDs per line cost 3.5 % of the kernel).
   const uint32_t nblk = gridDim.x;
   const uint32_t vb = (nblk % 8u == 0u) ? (blockIdx.x % 8u) * (nblk / 8u) + blockIdx.x / 8u : blockIdx.x;
-  const uint64_t gw = (uint64_t)vb * 16u + wave;
+  const uint32_t gw = vb * 16u + wave;
   const uint32_t mode = a.mode;
-  const uint64_t n = a.n_dev ? ld_const(a.n_dev, 0) : a.n_items;
-  auto oidx = [&](uint64_t i) -> uint64_t { return a.out_idx ? (uint64_t)a.out_idx[i] : i; }; // output slot
+  const uint32_t n = (uint32_t)(a.n_dev ? ld_const(a.n_dev, 0) : a.n_items);
+  auto oidx = [&](uint32_t i) -> uint32_t { return a.out_idx ? a.out_idx[i] : i; }; // output slot
   auto store_out = [&](uint32_t *p, uint32_t v) {
     if constexpr ((ABL & kRowsAblNtStore) != 0) __builtin_nontemporal_store(v, p);
     else *p = v;
   };
-  const uint64_t n_tasks = (QB == 4) ? (n + 3) / 4 : n;
+  const uint32_t n_tasks = (QB == 4) ? (n + 3) / 4 : n;
   // Group dealing, G = 2^a.gshift: in each whole round of nwaves * G tasks,
   // wave gw takes the G consecutive tasks [gw * G, gw * G + G), so its results
   // of a round are G consecutive outputs (G = 32: the wave writes whole 128-B
   // lines).  Tasks past the last whole round are dealt round-robin.
   const uint32_t gshift = a.gshift;
-  const uint64_t gmask = (1ull << gshift) - 1;
-  const uint64_t tail_base = n_tasks / (nwaves << gshift) * (nwaves << gshift);
-  const uint64_t jg = tail_base / nwaves; // tasks per wave dealt in groups
-  auto task_of = [&](uint64_t j) -> uint64_t { // the wave's j-th task
+  const uint32_t gmask = (1u << gshift) - 1;
+  const uint32_t tail_base = n_tasks / (nwaves << gshift) * (nwaves << gshift);
+  const uint32_t jg = tail_base / nwaves; // tasks per wave dealt in groups
+  auto task_of = [&](uint32_t j) -> uint32_t { // the wave's j-th task
     return j < jg ? ((((j >> gshift) * nwaves + gw) << gshift) | (j & gmask)) : tail_base + gw + (j - jg) * nwaves;
   };
-  auto next_task = [&](uint64_t t) -> uint64_t { // the wave's task after task t
+  auto next_task = [&](uint32_t t) -> uint32_t { // the wave's task after task t
     if (t >= tail_base) return t + nwaves;
     if (((t + 1) & gmask) != 0) return t + 1;
-    const uint64_t u = t + 1 + ((nwaves - 1) << gshift);
+    const uint32_t u = t + 1 + ((nwaves - 1) << gshift);
     return u < tail_base ? u : tail_base + gw;
   };
   // DYN: a wave's next task comes from the workgroup's LDS counter.  The
@@ -461,8 +521,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if (lane == 0) c = __hip_atomic_fetch_add(&s_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return c;
   };
-  auto dyn_task = [&](uint64_t c) -> uint64_t { return (((c / kDynRound) * nblk + vb) * kDynRound) | (c % kDynRound); };
-  uint64_t first_c = 0, first_task;
+  auto dyn_task = [&](uint32_t c) -> uint32_t { return (((c / kDynRound) * nblk + vb) * kDynRound) | (c % kDynRound); };
+  uint32_t first_c = 0, first_task;
   if constexpr (DYN) {
     first_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)dyn_grab());
     first_task = dyn_task(first_c);
@@ -471,7 +531,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   }
   if (first_task >= n_tasks) return;
 
-  auto synth = [&](uint64_t key, u32x4 (&buf)[4]) {
+  auto synth = [&](uint32_t key, u32x4 (&buf)[4]) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const uint32_t v = (uint32_t)key * 0x9E3779B1u + (uint32_t)b * 0x85EBCA6Bu + lane;
@@ -482,6 +542,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // crc0 of quarter hi of the row.
   auto quarter_crcs = [&](u32x4 (&buf)[4]) -> uint32_t {
     if constexpr ((ABL & kRowsAblNoTranspose) == 0) transpose(buf);
+    if constexpr ((ABL & (kRowsAblNoCompute | kRowsAblNoMerge)) == 0) return row_quarters(lds, buf, lsel, lsel1, upper);
     uint32_t s;
     if constexpr ((ABL & kRowsAblNoCompute) != 0) s = xor_fold(buf);
     else s = seg_crc(lds, buf, lsel);
@@ -493,32 +554,36 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // Item metadata (wave-uniform).  item must be < n.
     // The zlib seed A_first(0xFFFFFFFF) of the item's first row is a scalar
     // load from the global Tq table, issued here -- a task ahead of its use.
-    auto meta = [&](uint64_t item, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &nr,
+    // hd = bytes of the item's first row (1..4096; 0 for an empty item) after
+    // the z pad: row r starts at item offset r * 4096 + hd - 4096, so only row
+    // 0 can start before the item (when hd < 4096).
+    auto meta = [&](uint32_t item, uint64_t &p0, uint32_t &hd, uint32_t &len, uint32_t &z, uint32_t &nr,
                     uint32_t &seed) {
-      const uint64_t off = RAGGED ? ld_const(a.offsets, item) : item * a.stride;
+      const uint64_t off = RAGGED ? ld_const(a.offsets, item) : (uint64_t)item * a.stride;
       len = RAGGED ? ld_const(a.lengths, item) : a.len;
       if constexpr (RAGGED) {
         // a routed big body is empty here (launch_big_route computes it)
         if (len >= a.big_min && a.routed != nullptr) {
-          const uint64_t bi = a.out_idx ? (uint64_t)ld_const(a.out_idx, item) : item;
+          const uint32_t bi = a.out_idx ? ld_const(a.out_idx, item) : item;
           if ((ld_const(a.routed, bi >> 5) >> (bi & 31u)) & 1u) len = 0;
         }
       }
       p0 = (uint64_t)(uintptr_t)a.base + off;
       z = (uint32_t)(0u - (uint32_t)(p0 + len)) & 15u;
-      lp = (uint64_t)len + z;
+      const uint64_t lp = (uint64_t)len + z;
       const uint64_t rows_ = (lp + kRow - 1) / kRow;
       nr = rows_ ? (uint32_t)rows_ : 1u; // zero-length items: one fully masked row
+      hd = (uint32_t)(lp - (uint64_t)(nr - 1) * kRow);
       if constexpr ((ABL & kRowsAblLdsSeed) != 0)
-        seed = (uint32_t)(lp - (uint64_t)(nr - 1) * kRow); // resolved in compute
+        seed = hd; // resolved in compute
       else
-        seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, (uint32_t)(lp - (uint64_t)(nr - 1) * kRow));
+        seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, hd);
     };
-    auto issue = [&](uint64_t p0, uint64_t lp, uint32_t nr, uint32_t r, bool ok, uint64_t safe, u32x4 (&buf)[4]) {
+    auto issue = [&](uint64_t p0, uint32_t hd, uint32_t nr, uint32_t r, bool ok, uint64_t safe, u32x4 (&buf)[4]) {
       if constexpr ((ABL & kRowsAblNoLoad) != 0) {
-        synth(p0 + r, buf);
+        synth((uint32_t)p0 + r, buf);
       } else {
-        const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
+        const bool fp = r == 0 && hd < kRow; // a first row that starts before the item
         // One load sequence for every row (loads issued from two paths broke
         // the compiler's vmcnt accounting: the row just issued was waited for).
         // Whole rows: scalar row base + the lane's constant offsets.  A first
@@ -526,18 +591,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         // pieces before it read as zeros; invalid rows read nothing.
         uint64_t base;
         uint32_t off[4];
-        if (ok && rs >= 0 && (ABL & kRowsAblNoFastLoad) == 0) {
-          base = p0 + (uint64_t)rs;
+        if (ok && !fp && (ABL & kRowsAblNoFastLoad) == 0) {
+          base = p0 + (uint64_t)r * kRow + hd - kRow;
 #pragma unroll
           for (int b = 0; b < 4; ++b) off[b] = pofs + b * kQuarter;
         } else {
           base = ok ? (p0 & ~(uint64_t)15) : safe;
-          const int32_t d = ok ? (int32_t)(rs + (int64_t)(p0 & 15)) : INT32_MIN / 2;
+          const int32_t d = ok ? (int32_t)(r * kRow + hd) - (int32_t)kRow + (int32_t)(p0 & 15) : INT32_MIN / 2;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int32_t o = d + (int32_t)(pofs + b * kQuarter);
-            off[b] = o >= 0 ? (uint32_t)o : kOobOffset;
-          }
+          for (int b = 0; b < 4; ++b) // negative offsets (pieces before the item) -> kOobOffset: one v_min_u32
+            off[b] = min((uint32_t)(d + (int32_t)(pofs + b * kQuarter)), kOobOffset);
         }
         const __amdgpu_buffer_rsrc_t row = row_rsrc(base);
 #pragma unroll
@@ -549,7 +612,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // item, item = gw + (j0 + k) * nwaves) and stored 64 at a time: a per-row
     // store would make the compiler drain vmcnt (store-data WAR) every row.
     uint32_t outv = 0, ocount = 0;
-    uint64_t j0 = 0;
+    uint32_t j0 = 0;
     uint32_t sink = 0;
     auto flush = [&]() {
       if constexpr ((ABL & kRowsAblNoStore) == 0) {
@@ -566,8 +629,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     // DYN output: CRC of the task with counter index c into the LDS ring; the
     // wave completing a round stores the round's CRCs as one whole line.
-    auto dyn_out = [&](uint64_t c, uint32_t res) {
-      const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
+    auto dyn_out = [&](uint32_t c, uint32_t res) {
+      const uint32_t rnd = c / kDynRound, idx = c % kDynRound, slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots;
       uint32_t old = 0;
       if (lane == 0) {
@@ -578,8 +641,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      const uint64_t base = ((uint64_t)rnd * nblk + vb) * kDynRound;
-      const uint32_t cnt = (n_tasks - base < kDynRound) ? (uint32_t)(n_tasks - base) : kDynRound;
+      const uint32_t base = (rnd * nblk + vb) * kDynRound;
+      const uint32_t cnt = (n_tasks - base < kDynRound) ? n_tasks - base : kDynRound;
       if (old + 1u == cnt) { // this wave completed the round
         const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
         if constexpr ((ABL & kRowsAblNoStore) == 0) {
@@ -594,13 +657,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         j0 += cnt;
       }
     };
-    auto compute = [&](bool valid, uint64_t lp, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
-                       uint64_t cidx, u32x4 (&buf)[4]) {
-      const int64_t rs = (int64_t)lp - (int64_t)(nr - r) * (int64_t)kRow;
+    auto compute = [&](bool valid, uint32_t hd, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
+                       uint32_t cidx, u32x4 (&buf)[4]) {
+      const bool fp = r == 0 && hd < kRow;
       const bool last = r + 1 == nr;
-      if (rs < 0 || (last && z != 0)) {
-        // the body's first byte sits at row offset -rs (first row only)
-        const uint32_t front = rs < 0 ? (uint32_t)(-rs) : kRow;
+      if (fp || (last && z != 0)) {
+        // the body's first byte sits at row offset 4096 - hd (first row only)
+        const uint32_t front = fp ? kRow - hd : kRow;
         constexpr bool kNat = (ABL & kRowsAblNaturalOrder) != 0;
 #pragma unroll
         for (uint32_t b = 0; b < 4; ++b) {
@@ -638,9 +701,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     };
 
-    uint64_t c_item = first_task;
-    uint64_t c_p0, c_lp;
-    uint32_t c_len, c_z, c_nr, c_seed, c_r = 0;
+    uint32_t c_item = first_task;
+    uint64_t c_p0;
+    uint32_t c_lp, c_len, c_z, c_nr, c_seed, c_r = 0; // c_lp: the item's first-row bytes (hd)
     meta(c_item, c_p0, c_lp, c_len, c_z, c_nr, c_seed);
     const uint64_t safe = c_p0 & ~(uint64_t)15; // 16-B block holding this wave's first byte
     // Successor of task (item, r) with metadata nr: same item next row, or the
@@ -648,9 +711,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // (in-range) metadata and load from `safe`; their results are dropped.
     uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
     if constexpr (DYN) pend = dyn_grab();
-    uint64_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
-    auto succ = [&](bool ok, uint64_t item, uint32_t r, uint32_t nr, uint64_t &s_item, uint32_t &s_r,
-                    bool &s_ok, uint64_t &p0, uint64_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr,
+    uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
+    auto succ = [&](bool ok, uint32_t item, uint32_t r, uint32_t nr, uint32_t &s_item, uint32_t &s_r,
+                    bool &s_ok, uint64_t &p0, uint32_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr,
                     uint32_t &seed) {
       const bool adv = r + 1 < nr;
       if constexpr (DYN) {
@@ -680,7 +743,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
-        uint64_t m_item, m_p0, m_lp;
+        uint32_t m_item, m_lp;
+        uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
         bool m_ok;
         succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
@@ -704,14 +768,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     } else {
       // DEPTH = 2: the next two rows' loads are in flight while one computes.
       u32x4 bufA[4], bufB[4], bufC[4];
-      uint64_t n_item, n_p0, n_lp;
+      uint32_t n_item, n_lp;
+      uint64_t n_p0;
       uint32_t n_r, n_len, n_z, n_nr, n_seed;
       bool n_ok;
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
       succ(true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_p0, n_lp, n_len, n_z, n_nr, n_seed);
       issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) {
-        uint64_t m_item, m_p0, m_lp;
+        uint32_t m_item, m_lp;
+        uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
         bool m_ok;
         succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
@@ -756,13 +822,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     }
   } else {
     // QB = 4: group g = items [4g, 4g+4), quarter b <-> item 4g+b (len + pad <= 1 KiB).
-    const uint64_t ngroups = (n + 3) / 4;
-    auto quarter = [&](uint64_t g, int b) -> QuarterInfo {
+    const uint32_t ngroups = (n + 3) / 4;
+    auto quarter = [&](uint32_t g, int b) -> QuarterInfo {
       QuarterInfo r;
-      const uint64_t item = 4 * g + b;
+      const uint32_t item = 4 * g + b;
       const bool ok = item < n;
-      const uint64_t it = ok ? item : 0;
-      const uint64_t off = RAGGED ? ld_const(a.offsets, it) : it * a.stride;
+      const uint32_t it = ok ? item : 0;
+      const uint64_t off = RAGGED ? ld_const(a.offsets, it) : (uint64_t)it * a.stride;
       const uint32_t len = RAGGED ? ld_const(a.lengths, it) : a.len;
       r.len = ok ? len : 0u;
       r.p0 = a.base + off;
@@ -803,13 +869,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         aqm.sl = (hi == (uint32_t)b) ? seed : aqm.sl;
       }
     }
-    auto issue = [&](uint64_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) -> QuadMeta {
+    auto issue = [&](uint32_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) -> QuadMeta {
       QuarterInfo qi[4];
       QuadMeta qm;
       bool full = ok;
       qm.sl = 0;
       if (affine && ok && 4 * g + 4 <= n) {
-        const uint64_t gofs = 4 * g * a.stride;
+        const uint64_t gofs = (uint64_t)g * 4u * a.stride;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           qi[b] = aq[b];
@@ -847,7 +913,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
             const bool live = ok && qi[b].len != 0;
             base[b] = live ? (p & ~(uint64_t)15) : safe;
             const int32_t o = live ? (int32_t)(qi[b].vstart + (int64_t)(p & 15)) + (int32_t)pofs : -1;
-            off[b] = o >= 0 ? (uint32_t)o : kOobOffset;
+            off[b] = min((uint32_t)o, kOobOffset);
           }
         }
 #pragma unroll
@@ -857,10 +923,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     // Parked results: lane k = item 4 * (gw + (j0 + k / 4) * nwaves) + k % 4 (see QB = 1).
     uint32_t outv = 0, ocount = 0;
-    uint64_t j0 = 0;
+    uint32_t j0 = 0;
     // DYN output (see QB = 1): the 4 CRCs of group task c into the LDS ring; the
     // wave completing a round stores its (up to) 128 CRCs as two 256-B stores.
-    auto dyn_out4 = [&](uint64_t c, const uint32_t (&v)[4]) {
+    auto dyn_out4 = [&](uint32_t c, const uint32_t (&v)[4]) {
       constexpr uint32_t kW = kDynRound * 4;
       const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots + slot * kW;
@@ -873,10 +939,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      const uint64_t base = ((uint64_t)rnd * nblk + vb) * kDynRound; // first group of the round
+      const uint32_t base = (rnd * nblk + vb) * kDynRound; // first group of the round
       const uint32_t cnt = (ngroups - base < kDynRound) ? (uint32_t)(ngroups - base) : kDynRound;
       if (old + 1u == cnt) {
-        const uint64_t ibase = 4 * base;
+        const uint32_t ibase = 4 * base;
         const uint32_t nit = (n - ibase < kW) ? (uint32_t)(n - ibase) : kW;
         const uint32_t v0 = ring[lane], v1 = ring[64 + lane];
         if (lane < nit) store_out(a.out + oidx(ibase + lane), v0);
@@ -889,12 +955,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     };
     auto flush = [&]() {
-      const uint64_t item = 4 * task_of(j0 + lane / 4u) + (lane & 3u);
+      const uint32_t item = 4 * task_of(j0 + lane / 4u) + (lane & 3u);
       if (lane < ocount && item < n) a.out[oidx(item)] = outv;
       j0 += ocount / 4u;
       ocount = 0;
     };
-    auto compute = [&](const QuadMeta &qm, bool valid, uint64_t cidx, u32x4 (&buf)[4]) {
+    auto compute = [&](const QuadMeta &qm, bool valid, uint32_t cidx, u32x4 (&buf)[4]) {
       uint32_t zl = 0, zany = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -931,21 +997,21 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (ocount == 64u) flush();
       }
     };
-    uint64_t g = first_task;
+    uint32_t g = first_task;
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       QuadMeta c_qm = issue(g, true, safe, bufA);
       uint32_t pend = 0;
       if constexpr (DYN) pend = dyn_grab();
-      uint64_t c_c = first_c;
+      uint32_t c_c = first_c;
       bool c_ok = true; // the group being computed next is real
       // One exit, at the bottom (see QB = 1): a mid-body break made the
       // compiler drain vmcnt before the next group's loads on every step
       // (ISA: s_waitcnt vmcnt(0) ahead of the offset of the 4th quarter load).
       // Steps past the wave's last group load nothing and store nothing.
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
-        uint64_t ng, n_c = 0;
+        uint32_t ng, n_c = 0;
         if constexpr (DYN) {
           n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
           ng = dyn_task(n_c);
@@ -969,10 +1035,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
-      uint64_t gn = next_task(g);
+      uint32_t gn = next_task(g);
       n_qm = issue(gn < ngroups ? gn : g, gn < ngroups, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
-        const uint64_t g2 = next_task(gn);
+        const uint32_t g2 = next_task(gn);
         const bool ok2 = g2 < ngroups;
         const QuadMeta m_qm = issue(ok2 ? g2 : g, ok2, safe, fb);
         compute(c_qm, true, 0, cb);

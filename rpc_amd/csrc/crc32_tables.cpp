@@ -37,8 +37,8 @@ void build_lds_image_v2(uint32_t *img) {
     }
   }
   uint32_t nt[8][16];
-  for (uint32_t c = 0; c < 32; ++c) { // lo = c & 15
-    nibble_table(64u * (15u - (c & 15u)), nt);
+  for (uint32_t c = 0; c < 32; ++c) { // lo = c & 15; banks 16..31 add the first half-segment's A_32
+    nibble_table(64u * (15u - (c & 15u)) + (kTwoChains ? 32u * ((c >> 4) & 1u) : 0u), nt);
     for (int n = 0; n < 8; ++n)
       for (uint32_t nib = 0; nib < 16; ++nib)
         put(kLdsST1 + (n >> 1) * 4096 + nib * 256 + (n & 1) * 128 + c * 4, nt[n][nib]);

@@ -373,8 +373,8 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   const bool fits = n < (1ull << 27); // the packed kernel's metadata window: 8-B offsets in a 1 GiB buffer range
   const bool auto_frames = path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies;
   const bool packed = fits && (path == RPCCRC_RAGGED_PACKED || (auto_frames && !kAutoSplitFrames));
-  const bool split = !packed && n < 0xFFFFFFFFull && (path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
-  route = route && !packed && mode == kModeFinal && n < 0xFFFFFFFFull;
+  const bool split = !packed && n <= kMaxLaunchItems && (path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
+  route = route && !packed && mode == kModeFinal && n <= kMaxLaunchItems;
   ItemsArgs a = items_args(c, base, offsets, lengths, n, 0, 0, mode, out);
   if (packed) {
     const uint64_t ms = std::min<uint64_t>(kPackedMaxSlices, std::max<uint64_t>(8192, 4 * n));

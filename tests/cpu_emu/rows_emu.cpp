@@ -92,6 +92,8 @@ static void permlane32_swap(Wave x, Wave y) {
   for (int l = 0; l < 64; ++l) { x[l] = nx[l]; y[l] = ny[l]; }
 }
 
+static Wave g_chain_b; // two-chain mode: each lane's second chain value (row_chain -> merge_lo)
+
 // One 4 KiB row: P[b][lane] = the piece lane loaded in load b (already masked).
 // Returns the per-lane chain value after the transpose.
 static void row_chain(Piece P[4][64], Wave s_out) {
@@ -106,6 +108,18 @@ static void row_chain(Piece P[4][64], Wave s_out) {
   }
   for (int l = 0; l < 64; ++l) {
     uint32_t lane4 = (uint32_t)(l & 31) * 4u, lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);
+    if (kTwoChains) { // seg_crc2: slots 0-1 and 2-3 as two chains; s_out = a, s_out2 = b
+      uint32_t xa = P[0][l].d[0], xb = P[2][l].d[0];
+      for (int k = 0; k < 2; ++k)
+        for (int d = 0; d < 4; ++d) {
+          if (!k && !d) continue;
+          xa = slice4(xa, lsel) ^ P[k][l].d[d];
+          xb = slice4(xb, lsel) ^ P[k + 2][l].d[d];
+        }
+      s_out[l] = slice4(xa, lsel);
+      g_chain_b[l] = slice4(xb, lsel);
+      continue;
+    }
     uint32_t x = P[0][l].d[0];
     for (int k = 0; k < 4; ++k)
       for (int d = 0; d < 4; ++d) {
@@ -134,10 +148,34 @@ static uint32_t st1_map(uint32_t s, uint32_t lane) {
   }
   return r;
 }
+// swap_lanebit4 of the kernel: both results of v_permlane16_swap(v, v), then
+// upper lanes take the first, lower lanes the second.
+static void swap_lanebit4(const Wave v, Wave out) {
+  Wave a, b;
+  for (int l = 0; l < 64; ++l) { a[l] = v[l]; b[l] = v[l]; }
+  permlane16_swap(a, b);
+  for (int l = 0; l < 64; ++l) out[l] = (l & 16) ? a[l] : b[l];
+}
 static void merge_lo(Wave s) {
   static const int px1[4] = {1, 0, 3, 2}, px2[4] = {2, 3, 0, 1};
   Wave t;
-  for (int l = 0; l < 64; ++l) s[l] = st1_map(s[l], (uint32_t)l);
+  if (kTwoChains) { // merge_lo2: s = chain a, g_chain_b = chain b
+    Wave own, sel, other, t_own, t_other, back;
+    for (int l = 0; l < 64; ++l) {
+      const bool up = (l & 16) != 0;
+      own[l] = up ? s[l] : g_chain_b[l];
+      sel[l] = up ? g_chain_b[l] : s[l];
+    }
+    swap_lanebit4(sel, other);
+    for (int l = 0; l < 64; ++l) {
+      t_own[l] = st1_map(own[l], (uint32_t)l);
+      t_other[l] = st1_map(other[l], (uint32_t)l);
+    }
+    swap_lanebit4(t_other, back);
+    for (int l = 0; l < 64; ++l) s[l] = t_own[l] ^ back[l];
+  } else {
+    for (int l = 0; l < 64; ++l) s[l] = st1_map(s[l], (uint32_t)l);
+  }
   quad_perm(s, t, px1); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
   quad_perm(s, t, px2); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
   row_ror(s, t, 4); for (int l = 0; l < 64; ++l) s[l] ^= t[l];

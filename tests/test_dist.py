@@ -92,7 +92,7 @@ def _hip_worker(rank, world, port, q):
         torch.cuda.set_device(0)
         n, L = 30011, 1500  # uneven shards, partial rows
         lo, hi = shard_range(n, rank, world)
-        x = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        x = torch.empty((n * L + 7) // 8 * 8, dtype=torch.uint8, device="cuda:0")
         rpc_amd.fill_random(x, 0x5EED0005)  # every rank sees the same logical batch
         mine = rpc_amd.device_uniform(x[lo * L:hi * L], hi - lo, L).cpu().numpy().view(np.uint32)
         parts = [None] * world

@@ -130,8 +130,11 @@ def _server_outcome(raw: bytes) -> str:
     """What the reference server does with one frame on a fresh connection."""
     s = socket.create_connection(("127.0.0.1", PORT), timeout=30)
     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-    s.sendall(raw)
-    hdr = recv_exact(s, 12)
+    try:
+        s.sendall(raw)
+        hdr = recv_exact(s, 12)
+    except ConnectionResetError:  # closed with our bytes unread: an RST instead of a FIN
+        hdr = b""
     s.close()
     if len(hdr) < 12:
         return "closed"

@@ -475,7 +475,7 @@ def test_device_batch_big_bodies_route(path, misalign):
     perm = np.random.default_rng(misalign).permutation(len(lens))
     lens_p = np.array(lens, dtype=np.uint32)[perm]
     offs_p = offs[perm]
-    base = torch.empty(int(offs[-1]) + lens[-1] + 16, dtype=torch.uint8, device=DEV)
+    base = torch.empty((int(offs[-1]) + lens[-1] + 16 + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
     rpc_amd.fill_random(base, 0xB16B0D1E + misalign)
     rpc_amd.set_ragged_path(path)
     try:

@@ -27,6 +27,32 @@ for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests_all) run tests_all 900 python -u -m pytest tests -m gpu -q -rfE --timeout 120 --timeout-method thread ;;
+    tests_sel) run tests_sel 600 python -u -m pytest ${TESTS_SEL:-tests} -m gpu -q -rfE --timeout 120 --timeout-method thread ;;
+    prof_cfgs)
+           for c in ${PROF_CFGS:-c2}; do
+             run prof_$c 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o run --output-format csv -- \
+                 python3 bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive || exit 1
+           done ;;
+    power_sweep)
+           run ps_ns20 300 python bench.py --steps 20 --no-cpu-baseline --no-host-inclusive &&
+           run ps_ns160 300 python bench.py --steps 160 --no-cpu-baseline --no-host-inclusive &&
+           run ps_ns800 300 python bench.py --steps 800 --no-cpu-baseline --no-host-inclusive &&
+           run ps_c3_3 300 python bench.py --config c3 --steps 3 --no-cpu-baseline --no-host-inclusive &&
+           run ps_c3_20 300 python bench.py --config c3 --steps 20 --no-cpu-baseline --no-host-inclusive ;;
+    ablate_r02)
+           V=qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl1028_d1,qb1_pair1_nt1_abl1027_d1,qb1_pair1_nt1_abl1025_d1,qb1_pair1_nt1_abl1026_d1,qb1_pair1_nt1_abl1056_d1,qb1_pair1_nt1_abl1059_d1
+           for c in ${ABL_CFGS:-ns u3k u2k}; do run ablate_r02_$c 600 python tools/probe.py --mode ablate --rounds 3 --config $c --only $V || exit 1; done
+           run lib_r02 300 python tools/probe.py --mode lib --rounds 3 ;;
+    pmc_mix)
+           for c in ${PMC_CFGS:-ns c2}; do
+             run pmcmix1_$c 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+                 -d "$OUT/pmcmix1_$c" -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive || exit 1
+             run pmcmix2_$c 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
+                 -d "$OUT/pmcmix2_$c" -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive || exit 1
+           done ;;
+    bench_c3) run bench_c3 600 python bench.py --config c3 --no-cpu-baseline --no-host-inclusive ;;
+    bench_scalar) run bench_scalar 300 tools/scalar_bench oracle/_ref/libref_crc.so ;;
     bench) run bench 600 python bench.py ;;
     probe) run probe 600 python tools/probe.py ;;
     ablate) run ablate 600 python tools/probe.py --mode ablate --rounds 3 ;;

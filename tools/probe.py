@@ -86,6 +86,8 @@ def ablate_variants(w, a):
               (1, 1, 1, 259, 1), (1, 1, 1, 275, 1)]
     combos += [(1, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(1, 1, 1, 3, 1, 5), (1, 1, 1, 19, 1, 5)]
     combos += [(1, 1, 1, 1024, 1), (1, 1, 1, 1027, 1), (1, 1, 1, 1043, 1)]  # DYN (+ memory only)
+    # DYN: merge only / chain only / compute only / no transpose / memory only without transpose
+    combos += [(1, 1, 1, 1025, 1), (1, 1, 1, 1026, 1), (1, 1, 1, 1028, 1), (1, 1, 1, 1056, 1), (1, 1, 1, 1059, 1)]
     combos += [(1, 1, 1, 3072, 1), (1, 1, 1, 1040, 1)]  # DYN with NT stores / no stores
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),

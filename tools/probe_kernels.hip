@@ -68,6 +68,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_times(const uin
   V(4, 1, 0, 1) V(4, 0, 0, 1) V(4, 1, 3, 1) V(4, 1, 4, 1) V(4, 1, 6, 1) V(4, 1, 0, 2) V(4, 1, 3, 2)
   V(1, 1, 259, 1) V(1, 1, 275, 1) V(1, 1, 512, 1) V(4, 1, 512, 1)
   V(1, 1, 1024, 1) V(1, 1, 1027, 1) V(1, 1, 1043, 1) V(1, 1, 1536, 1) V(4, 1, 1024, 1) V(4, 1, 1536, 1)
+  V(1, 1, 1025, 1) V(1, 1, 1026, 1) V(1, 1, 1028, 1) V(1, 1, 1056, 1) V(1, 1, 1059, 1)
   V(4, 1, 1027, 1) V(4, 1, 1043, 1) V(4, 1, 1028, 1) V(1, 1, 3072, 1) V(4, 1, 3072, 1) V(1, 1, 1040, 1) V(4, 1, 1040, 1)
   return -22;
 }
