@@ -332,12 +332,20 @@ def self_launch(args) -> int:
     code.  Runs before torch is imported here, so this parent never touches a GPU."""
     import subprocess
 
-    port = args.master_port or free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
-    return subprocess.call(cmd, env=env)
+    rc = 1
+    for attempt in range(2):  # a free port can be taken between our probe and the launcher's bind
+        port = args.master_port or free_port()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        t0 = time.perf_counter()
+        rc = subprocess.call(cmd, env=env)
+        if rc == 0 or args.master_port or time.perf_counter() - t0 > 30:
+            break
+        print(f"bench: launcher exited {rc} within {time.perf_counter() - t0:.1f} s; retrying on a new port",
+              file=sys.stderr)
+    return rc
 
 
 def main():
