@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (multi-thread leg)")
     p.add_argument("--master-port", type=int, default=0, help="N>1 self-launch: rendezvous port (0 = pick a free one)")
     p.add_argument("--no-scalar-latency", action="store_true")
+    p.add_argument("--no-live-traffic", action="store_true",
+                   help="skip the two rocprofv3 PMC child passes (roofline.traffic from profiles/traffic.json)")
     p.add_argument("--prewarm-s", type=float, default=0.5,
                    help="untimed steps before the W warmup steps until this much time has passed: the GPU "
                         "clock ramps over the first ~20 launches of sustained load (DESIGN.md 5)")
@@ -141,6 +143,11 @@ def _loguniform_lengths(n, seed, lo=64, hi=65536):
     u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
     ln = np.floor(lo * np.exp(u * np.log(hi / lo))).astype(np.int64)
     return np.clip(ln, lo, hi).astype(np.uint32)
+
+
+def log(msg: str):
+    """Progress on stderr (a silent minute looks like a hang to the GPU harness)."""
+    print(f"bench: {msg}", file=sys.stderr, flush=True)
 
 
 def cpu_model():
@@ -318,6 +325,56 @@ def load_traffic(cfg: str):
         return None
 
 
+def live_traffic(args, algo_bytes: int):
+    """HBM bytes per launch of the dominant kernel, measured in this run: two
+    rocprofv3 PMC passes (FETCH_SIZE, then WRITE_SIZE -- separate runs, as
+    MI355X_MICROARCH.md prescribes) over a short child bench of the same config,
+    corrected as that guide says: gfx950 FETCH_SIZE counts half the bytes of a
+    wide streaming read (x 2), both are in KiB (x 1024).  The rows kernel also
+    runs tiny launches (the big-body route's empty chunk pass): only dispatches
+    within half of the largest count.  Falls back to the committed summary."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="rpccrc_pmc_")
+    vals = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "3",
+                   "--warmup", "1", "--prewarm-s", "0", "--no-cpu-baseline", "--no-host-inclusive",
+                   "--no-live-traffic"] + (["--ragged-path", args.ragged_path] if args.ragged_path != "auto" else [])
+            try:
+                p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 --pmc {counter} timed out"
+            if p.returncode != 0:
+                return None, f"rocprofv3 --pmc {counter} rc={p.returncode}: {(p.stderr or '')[-200:]}"
+            per = {}
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for r in csv.DictReader(open(f)):
+                    if r["Counter_Name"] == counter and "crc32_rows_kernel" in r["Kernel_Name"]:
+                        per[(f, r["Dispatch_Id"])] = per.get((f, r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+            if not per:
+                return None, f"no {counter} rows for crc32_rows_kernel"
+            v = sorted(per.values())
+            vals[counter] = statistics.median([x for x in v if x >= 0.5 * v[-1]])
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    hbm = 2.0 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024
+    return {"hbm_bytes_per_launch": hbm, "over_algorithmic": round(hbm / algo_bytes, 4),
+            "fetch_size_kib": vals["FETCH_SIZE"], "write_size_kib": vals["WRITE_SIZE"]}, \
+        "live: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this config (2 x FETCH_SIZE + WRITE_SIZE, KiB)"
+
+
 def free_port() -> int:
     import socket
 
@@ -417,19 +474,33 @@ def main():
     extra = {}
     cpu = None
     if rank == 0 and world == 1:
+        log("stream-read probe")
         extra["stream_read_probe"] = stream_read_probe(w)
         if not args.no_host_inclusive:
+            log("host-inclusive batch")
             extra["host_inclusive"] = host_inclusive(w)
             if w.kind == "uniform":
+                log("receive ring")
                 extra["rx_ring"] = rx_ring_probe()
         if not args.no_scalar_latency and not args.no_host_inclusive:
+            log("scalar latency")
             extra["scalar_latency"] = scalar_latency_probe()
         if not args.no_cpu_baseline:
+            log("CPU baseline (reference crc.c)")
             cpu = cpu_baseline(w, args.cpu_seconds)
 
     if rank == 0:
         achieved = w.algo_bytes / kernel_s / 1e9
-        traffic = load_traffic(args.config)
+        traffic_rec, traffic_src = None, "not measured"
+        if world == 1 and not args.no_live_traffic:
+            log("measuring HBM traffic (two rocprofv3 PMC passes)")
+            traffic_rec, traffic_src = live_traffic(args, w.algo_bytes)
+        if traffic_rec is not None:
+            traffic = traffic_rec["hbm_bytes_per_launch"]
+        else:
+            traffic = load_traffic(args.config)
+            if traffic is not None:
+                traffic_src = f"committed profiles/traffic.json ({traffic_src})"
         line = {
             "metric": METRIC,
             "value": round(total_bytes * args.steps / tmax / GiB, 2),
@@ -459,6 +530,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / (HBM_PEAK_BPS / 1e9), 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "traffic_detail": traffic_rec,
                 "kernel": {"uniform": "crc32_rows_kernel",
                            "ragged": "crc32_packed_kernel (+count/scan/plan)" if args.ragged_path == "packed"
                            else "crc32_rows_kernel",

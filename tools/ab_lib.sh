@@ -15,7 +15,7 @@ for i in $(seq 1 "$ROUNDS"); do
       if [ "$lib" = head ]; then unset RPCCRC_LIB; else export RPCCRC_LIB=$PWD/abtest/$lib.so; fi
       cfg=${c%%:*}; extra=""; [ "$cfg" != "$c" ] && extra=$(echo "${c#*:}" | tr ',' ' ')
       tag=$(echo "$c" | tr -c 'a-zA-Z0-9_\n' '_'); ltag=$(echo "$l" | tr -c 'a-zA-Z0-9_\n' '_')
-      timeout -k 10 300 env $envs python bench.py --config "$cfg" $extra --no-cpu-baseline --no-host-inclusive > "$OUT/${tag}_${ltag}_$i.log" 2>&1
+      timeout -k 10 300 env $envs python bench.py --config "$cfg" $extra --no-cpu-baseline --no-host-inclusive --no-live-traffic > "$OUT/${tag}_${ltag}_$i.log" 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "FAIL $c $l rc=$rc"; tail -3 "$OUT/${tag}_${ltag}_$i.log"; [ $rc -ge 124 ] && exit $rc; continue; fi
       python3 - "$OUT/${tag}_${ltag}_$i.log" "$c" "$l" <<'PY'

@@ -32,14 +32,14 @@ for s in $STEPS; do
     prof_cfgs)
            for c in ${PROF_CFGS:-c2}; do
              run prof_$c 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o run --output-format csv -- \
-                 python3 bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive || exit 1
+                 python3 bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
            done ;;
     power_sweep)
-           run ps_ns20 300 python bench.py --steps 20 --no-cpu-baseline --no-host-inclusive &&
-           run ps_ns160 300 python bench.py --steps 160 --no-cpu-baseline --no-host-inclusive &&
-           run ps_ns800 300 python bench.py --steps 800 --no-cpu-baseline --no-host-inclusive &&
-           run ps_c3_3 300 python bench.py --config c3 --steps 3 --no-cpu-baseline --no-host-inclusive &&
-           run ps_c3_20 300 python bench.py --config c3 --steps 20 --no-cpu-baseline --no-host-inclusive ;;
+           run ps_ns20 300 python bench.py --steps 20 --no-cpu-baseline --no-host-inclusive --no-live-traffic &&
+           run ps_ns160 300 python bench.py --steps 160 --no-cpu-baseline --no-host-inclusive --no-live-traffic &&
+           run ps_ns800 300 python bench.py --steps 800 --no-cpu-baseline --no-host-inclusive --no-live-traffic &&
+           run ps_c3_3 300 python bench.py --config c3 --steps 3 --no-cpu-baseline --no-host-inclusive --no-live-traffic &&
+           run ps_c3_20 300 python bench.py --config c3 --steps 20 --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
     ablate_r02)
            V=qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl1028_d1,qb1_pair1_nt1_abl1027_d1,qb1_pair1_nt1_abl1025_d1,qb1_pair1_nt1_abl1026_d1,qb1_pair1_nt1_abl1056_d1,qb1_pair1_nt1_abl1059_d1
            for c in ${ABL_CFGS:-ns u3k u2k}; do run ablate_r02_$c 600 python tools/probe.py --mode ablate --rounds 3 --config $c --only $V || exit 1; done
@@ -47,9 +47,9 @@ for s in $STEPS; do
     pmc_mix)
            for c in ${PMC_CFGS:-ns c2}; do
              run pmcmix1_$c 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
-                 -d "$OUT/pmcmix1_$c" -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive || exit 1
+                 -d "$OUT/pmcmix1_$c" -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
              run pmcmix2_$c 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
-                 -d "$OUT/pmcmix2_$c" -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive || exit 1
+                 -d "$OUT/pmcmix2_$c" -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
            done ;;
     bench_c3) run bench_c3 600 python bench.py --config c3 --no-cpu-baseline --no-host-inclusive ;;
     bench_scalar) run bench_scalar 300 tools/scalar_bench oracle/_ref/libref_crc.so ;;
@@ -61,7 +61,7 @@ for s in $STEPS; do
     ablate_c1) run ablate_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 --only qb4_pair1_nt1_abl0_d1,qb4_pair1_nt1_abl3_d1,qb4_pair1_nt1_abl4_d1,qb4_pair1_nt1_abl0_d2 ;;
     bench_c1) run bench_c1 600 python bench.py --config c1 --no-cpu-baseline --no-host-inclusive ;;
     bench_c2) run bench_c2 600 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive ;;
-    bench_c2_rows) run bench_c2_rows 600 python bench.py --config c2 --ragged-path rows --no-cpu-baseline --no-host-inclusive ;;
+    bench_c2_rows) run bench_c2_rows 600 python bench.py --config c2 --ragged-path rows --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
     timeline) run timeline 300 python tools/probe.py --mode timeline --reps 3 ;;
     timeline_c1) run timeline_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 ;;
     ablate_mem) run ablate_mem 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl19_d1,qb1_pair1_nt1_abl259_d1,qb1_pair1_nt1_abl275_d1 ;;
@@ -84,28 +84,28 @@ for s in $STEPS; do
                -d "$OUT/pmcpacked" -o run --output-format csv -- python3 tools/probe.py --mode packed --rounds 1 --reps 2 --shapes 4096x1M,1024x1M ;;
     c4_chunks)
            for k in ${C4_CHUNKS:-0 1024 256 64 32}; do
-             run c4_chunk$k 300 python bench.py --config c4 --chunk-kib $k --no-cpu-baseline --no-host-inclusive --steps 10 || exit 1
+             run c4_chunk$k 300 python bench.py --config c4 --chunk-kib $k --no-cpu-baseline --no-host-inclusive --no-live-traffic --steps 10 || exit 1
            done ;;
     prof_c4)
            for k in ${C4_PROF_CHUNKS:-1024 64}; do
              run prof_c4_$k 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_c4_$k" -o run --output-format csv -- \
-               python3 bench.py --config c4 --chunk-kib $k --steps 10 --warmup 3 --prewarm-s 0.2 --no-cpu-baseline --no-host-inclusive || exit 1
+               python3 bench.py --config c4 --chunk-kib $k --steps 10 --warmup 3 --prewarm-s 0.2 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
            done ;;
     packed) run packed 600 python tools/probe.py --mode packed --rounds 3 --reps 5 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-               python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive ;;
+               python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-               python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive &&
+               python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive --no-live-traffic &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-               python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive ;;
+               python3 bench.py --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
     pmc_cfgs)
            for c in ${PMC_CFGS:-c1 c2 c4}; do
              run pmc_fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$c" -o run --output-format csv -- \
-                 python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive || exit 1
+                 python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
              run pmc_write_$c 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$c" -o run --output-format csv -- \
-                 python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive || exit 1
+                 python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
            done ;;
     pmcprobe)
            V=qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl6_d1,qb1_pair1_nt1_abl4_d1,qb1_pair1_nt1_abl0_d2
