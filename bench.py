@@ -539,6 +539,11 @@ def main():
                 "avg_launch_us": round(kernel_s * 1e6, 2),
                 "median_launch_us": round(median_s * 1e6, 2),
                 "algo_bytes_per_launch": w.algo_bytes,
+                # the same achieved rate against a streaming read
+                # of the same buffer on the same GPU (non-temporal, the rows
+                # kernel's load shape), measured in this run.
+                "frac_of_stream_read": (round(achieved / extra["stream_read_probe"]["coalesced_nt1_GBps"], 4)
+                                        if "stream_read_probe" in extra else None),
             },
             "cpu_baseline": cpu,
             "prewarm": {"seconds": args.prewarm_s, "steps": prewarm_steps},

@@ -1,6 +1,7 @@
 // rpc_amd/csrc/crc32_tables.cpp -- builds the LDS image and the Tq table once
 // per device context (host code; uploaded to HBM, copied to LDS per workgroup).
 #include "crc32_gf2.h"
+#include "crc32_kernels.h"
 #include "crc32_layout.h"
 
 #include <string.h>
@@ -57,6 +58,13 @@ void build_lds_image_v2(uint32_t *img) {
       for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsZI2 + (z - 1) * 512 + n * 64 + nib * 4, nt[n][nib]);
   }
   for (uint32_t k = 0; k <= 256; ++k) put(kLdsTQ16 + 4 * k, gf2_shift_bytes(0xFFFFFFFFu, 16ull * k));
+}
+
+void build_scalar_tab(uint32_t *tab) {
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t v = 0; v < 256; ++v) tab[256 * k + v] = crc_slice_entry(k, v);
+  for (uint32_t k = kScalarNibK0; k < kScalarNibK0 + 10; ++k)
+    nibble_table(1u << k, reinterpret_cast<uint32_t(*)[16]>(tab + 1024 + (k - kScalarNibK0) * 128));
 }
 
 void build_tq(uint32_t *tq) {

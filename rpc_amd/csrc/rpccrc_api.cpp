@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -191,7 +192,9 @@ class ObjPool {
 struct ScalarCtx {
   hipStream_t stream = nullptr;
   uint8_t *pin = nullptr;   // pinned input staging, device-readable (zero-copy)
-  uint32_t *pout = nullptr; // pinned result
+  uint32_t *pout = nullptr; // pinned result (rows kernel path)
+  uint64_t *pres = nullptr; // pinned {crc, seq} of the one-wave kernel (polled)
+  uint32_t seq = 0;
   uint8_t *dbuf = nullptr;  // device staging for large bodies
   size_t dcap = 0;
 };
@@ -223,6 +226,7 @@ struct DeviceCtx {
   uint4 *img = nullptr; // LDS table image (rows kernel layout, 155 KiB)
   uint32_t *tq = nullptr;
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
+  uint4 *scalar_tab = nullptr; // one-wave scalar kernel's table image (kScalarTabWords)
   int status = RPCCRC_ENODEV;
   char name[128] = {0};
   char arch[64] = {0};
@@ -283,8 +287,9 @@ void init_device(int dev) {
     c.status = RPCCRC_ENODEV;
     return;
   }
-  std::vector<uint32_t> img(kLdsBytesV2 / 4), tq(kTqEntries), nib(kShiftNibWords);
+  std::vector<uint32_t> img(kLdsBytesV2 / 4), tq(kTqEntries), nib(kShiftNibWords), stab(kScalarTabWords);
   build_tq(tq.data());
+  build_scalar_tab(stab.data());
   uint32_t sq = kX0 >> 8; // x^8 (one zero byte); squared: x^(8 * 2^k)
   for (uint32_t k = 0; k < 64; ++k) {
     for (uint32_t i = 0; i < 8; ++i)
@@ -298,12 +303,14 @@ void init_device(int dev) {
   e = (e == hipSuccess) ? hipMalloc(&c.img, kLdsBytesV2) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.scalar_tab, kScalarTabWords * 4) : e;
   if (e == hipSuccess) {
     build_lds_image_v2(img.data());
     e = hipMemcpy(c.img, img.data(), kLdsBytesV2, hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c.scalar_tab, stab.data(), kScalarTabWords * 4, hipMemcpyHostToDevice);
   (void)hipSetDevice(prev);
   c.ws = new BlockPool(false, 1ull << 30);
   c.pin = new BlockPool(true, 256ull << 20);
@@ -583,8 +590,49 @@ int scalar_ctx_init(ScalarCtx &t) {
   if (t.stream) return RPCCRC_OK;
   RPCCRC_TRY(hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking));
   RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.pout), 64, hipHostMallocDefault));
+  // Coherent: the host polls this word while the kernel may still be running.
+  RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.pres), 64, hipHostMallocCoherent));
+  *reinterpret_cast<volatile uint64_t *>(t.pres) = 0;
   RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.pin), kScalarZeroCopyMax, hipHostMallocDefault));
   return RPCCRC_OK;
+}
+
+// Bodies <= kScalarMaxLen: the one-wave kernel, and the host polls the
+// pinned result word for this call's sequence number -- no stream
+// synchronisation (~3 us less per call: tools/latency_probe.hip,
+// profiles/r02/r02n_*).  A call whose result has not arrived after
+// kScalarSpinNs falls back to hipStreamSynchronize, which also surfaces a
+// device error.
+constexpr uint64_t kScalarSpinNs = 200000;
+
+uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+uint32_t scalar_small(const DeviceCtx &c, ScalarCtx &t, const uint8_t *src, uint32_t len) {
+  const uint32_t vbytes = 64u << scalar_seg_log2(len);
+  if (len) memcpy(t.pin + (vbytes - len), src, len);
+  const uint32_t seq = ++t.seq == 0 ? ++t.seq : t.seq; // 0 is the word's initial value
+  if (launch_scalar(t.pin, len, c.scalar_tab, c.tq, t.pres, seq, t.stream) != hipSuccess)
+    die("kernel launch", RPCCRC_EIO);
+  const volatile uint64_t *res = t.pres;
+  uint64_t v = *res;
+  if ((uint32_t)(v >> 32) != seq) {
+    const uint64_t t0 = mono_ns();
+    for (uint32_t spin = 1;; ++spin) {
+      v = *res;
+      if ((uint32_t)(v >> 32) == seq) break;
+      if ((spin & 255u) == 0 && mono_ns() - t0 > kScalarSpinNs) {
+        if (hipStreamSynchronize(t.stream) != hipSuccess) die("stream sync", RPCCRC_EIO);
+        v = *res;
+        if ((uint32_t)(v >> 32) != seq) die("scalar result", RPCCRC_EIO);
+        break;
+      }
+    }
+  }
+  return (uint32_t)v;
 }
 
 // One CRC through the GPU.  The context (stream + staging) is borrowed from
@@ -597,6 +645,11 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
   ScalarCtx *t = c->scalar->acquire();
   if ((rc = scalar_ctx_init(*t))) die("scalar context", rc);
   const uint8_t *src = static_cast<const uint8_t *>(data);
+  if (len <= kScalarMaxLen) {
+    const uint32_t r = scalar_small(*c, *t, src, len);
+    c->scalar->release(t);
+    return r;
+  }
   if (len <= kScalarZeroCopyMax) {
     memcpy(t->pin, src, len);
     rc = items(*c, t->pin, nullptr, nullptr, 1, 0, len, kModeFinal, t->pout, 1, t->stream);

@@ -75,6 +75,21 @@ def test_drop_in_frames(golden):
         assert rpc_amd.rpc_crc32_verify(body, int.from_bytes(hdr[8:12], "big"))
 
 
+def test_drop_in_one_wave_kernel_lengths():
+    """Bodies <= 4 KiB take the one-wave scalar kernel (crc32_scalar.hip): every
+    length 0..1100, every segment-size boundary up to 4 KiB and past it (rows
+    path), each right after a 4 KiB body of 0xFF so stale staging bytes before
+    the body must be masked."""
+    lens = list(range(0, 1101)) + [b + d for b in (2048, 4096) for d in (-65, -64, -63, -1, 0, 1, 63, 64, 65)]
+    lens += [65535, 65536, 65537]
+    ff = b"\xff" * 4096
+    want_ff = oracle.crc32(ff)
+    for n in lens:
+        data = oracle.splitmix_bytes(n, 0x5CA1 + n) if n else b""
+        assert rpc_amd.rpc_crc32(ff) == want_ff
+        assert rpc_amd.rpc_crc32(data) == oracle.crc32(data), n
+
+
 def test_drop_in_thread_safety():
     rng = np.random.default_rng(3)
     bodies = [rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes() for _ in range(400)]
