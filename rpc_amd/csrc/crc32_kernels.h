@@ -68,13 +68,8 @@ constexpr uint32_t kShiftNibWords = 64u * 8u * 16u; // 32 KiB: the chunk combine
 // ---- drop-in scalar calls (crc32_scalar.hip) ------------------
 // One wave CRCs one body of <= kScalarMaxLen bytes from pinned host staging
 // (the body right-aligned at offset 64 * 2^scalar_seg_log2(len) - len) and
-// stores {crc, seq} (crc in the low half) to pinned `result`.  Its table
-// image (kScalarTabWords words): T_k[256] slice-by-4 tables, k = 0..3, then
-// NIB[k - kScalarNibK0][i][j] = A_{2^k bytes}(j << 4i) for k = 2..11.
-constexpr uint32_t kScalarMaxLen = 4096;
-constexpr uint32_t kScalarNibK0 = 2;
-constexpr uint32_t kScalarTabWords = 1024 + 10 * 128;
-void build_scalar_tab(uint32_t *tab /* kScalarTabWords */);
+// stores {crc, seq} (crc in the low half) to pinned `result`.  Table image:
+// crc32_layout.h (kScalarTabWords).
 uint32_t scalar_seg_log2(uint32_t len);
 hipError_t launch_scalar(const uint8_t *stage, uint32_t len, const uint4 *tab, const uint32_t *tq, uint64_t *result,
                          uint32_t seq, hipStream_t stream);

@@ -57,4 +57,13 @@ void build_lds_image_v2(uint32_t *img /* kLdsBytesV2 bytes */);
 // Host-side builder (crc32_tables.cpp).
 void build_tq(uint32_t *tq /* kTqEntries */);
 
+// One-wave scalar kernel (crc32_scalar.hip): bodies of <= kScalarMaxLen
+// bytes.  Table image of kScalarTabWords words: T_k[256] slice-by-4 tables,
+// k = 0..3, then NIB[k - kScalarNibK0][i][j] = A_{2^k bytes}(j << 4i) for
+// k = 2..11.
+constexpr uint32_t kScalarMaxLen = 4096;
+constexpr uint32_t kScalarNibK0 = 2;
+constexpr uint32_t kScalarTabWords = 1024 + 10 * 128;
+void build_scalar_tab(uint32_t *tab /* kScalarTabWords */);
+
 } // namespace rpccrc

@@ -343,6 +343,11 @@ constexpr int kRowsAblNoImage = 256;    // no LDS image copy (timing only; with 
 // with the wave's task count; times = a.offsets (unused by uniform batches).
 constexpr int kRowsAblTimes = 512;
 constexpr int kRowsAblNtStore = 2048; // non-temporal CRC stores (DYN paths; exact)
+// QB = 1 software pipeline over rows (chain of row r+1 beside the merge of row r).
+#ifndef RPCCRC_ROWS_PIPE
+#define RPCCRC_ROWS_PIPE 1
+#endif
+constexpr bool kRowsPipe = RPCCRC_ROWS_PIPE != 0;
 
 namespace rows {
 
@@ -657,8 +662,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         j0 += cnt;
       }
     };
-    auto compute = [&](bool valid, uint32_t hd, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
-                       uint32_t cidx, u32x4 (&buf)[4]) {
+    auto fix_row = [&](uint32_t hd, uint32_t z, uint32_t nr, uint32_t r, u32x4 (&buf)[4]) {
       const bool fp = r == 0 && hd < kRow;
       const bool last = r + 1 == nr;
       if (fp || (last && z != 0)) {
@@ -671,14 +675,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           fix_quarter<kNat>(buf[b], lane, fb, (b == 3 && last) ? z : 0u);
         }
       }
-      const uint32_t v = quarter_crcs(buf);
-      RowMerge m;
-      if constexpr ((ABL & kRowsAblNoMerge) == 0) {
-        m = merge_row(lds, v, W, dl);
-      } else {
-        m.crc = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-        m.rwu = W;
-      }
+    };
+    // Horner step and result of a row whose merge is done.
+    auto finish = [&](bool valid, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed, uint32_t cidx,
+                      RowMerge m) {
+      const bool last = r + 1 == nr;
       // Horner over rows: A_4096(W), or the zlib seed on the item's first row.
       if constexpr ((ABL & kRowsAblLdsSeed) != 0) {
         if (r == 0) {
@@ -699,6 +700,19 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           if (valid) park(res);
         }
       }
+    };
+    auto compute = [&](bool valid, uint32_t hd, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
+                       uint32_t cidx, u32x4 (&buf)[4]) {
+      fix_row(hd, z, nr, r, buf);
+      const uint32_t v = quarter_crcs(buf);
+      RowMerge m;
+      if constexpr ((ABL & kRowsAblNoMerge) == 0) {
+        m = merge_row(lds, v, W, dl);
+      } else {
+        m.crc = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        m.rwu = W;
+      }
+      finish(valid, len, z, nr, r, seed, cidx, m);
     };
 
     uint32_t c_item = first_task;
@@ -739,7 +753,58 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // half the iterations).  Trailing steps past the wave's last task run on
     // invalid tasks (c_ok false): safe loads, no result parked.
     bool c_ok = true;
-    if constexpr (DEPTH == 1) {
+    // Ragged batches only: C2 -1.6 %, while uniform batches (north star
+    // +-0.5 %, C4's chunks +0.6 %) keep the plain loop
+    // (profiles/r02/r02r_rows_pipeline_ab.txt).
+    constexpr bool kPipe = kRowsPipe && RAGGED && !kTwoChains &&
+                           (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose)) == 0;
+    if constexpr (DEPTH == 1 && kPipe) {
+      // Software pipeline over rows: one step issues row M's loads, runs row
+      // C's edge fix, transpose and chain, and merges row P (the row before C,
+      // whose chain the previous step computed).  C's chain and P's merge are
+      // independent and share one basic block, so the scheduler overlaps P's
+      // dependent merge lookups with C's chain.  Rows still finish in order
+      // (Horner across rows needs that).
+      u32x4 bufA[4], bufB[4];
+      issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
+      bool p_ok = false; // no row pending before the first step
+      uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_chain = 0;
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
+        uint32_t m_item, m_lp;
+        uint64_t m_p0;
+        uint32_t m_r, m_len, m_z, m_nr, m_seed;
+        bool m_ok;
+        succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
+        issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
+        fix_row(c_lp, c_z, c_nr, c_r, cb);
+        transpose(cb);
+        const uint32_t ch = seg_crc(lds, cb, lsel);
+        const RowMerge pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
+        finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, pm);
+        p_ok = c_ok;
+        p_len = c_len;
+        p_z = c_z;
+        p_nr = c_nr;
+        p_r = c_r;
+        p_seed = c_seed;
+        p_c = c_c;
+        p_chain = ch;
+        c_c = m_c;
+        c_ok = m_ok;
+        c_seed = m_seed;
+        c_item = m_item;
+        c_r = m_r;
+        c_p0 = m_p0;
+        c_lp = m_lp;
+        c_len = m_len;
+        c_z = m_z;
+        c_nr = m_nr;
+      };
+      do {
+        step(bufA, bufB);
+        step(bufB, bufA);
+      } while (p_ok);
+    } else if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {

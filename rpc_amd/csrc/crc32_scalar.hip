@@ -21,6 +21,7 @@
 //           {crc, seq} to pinned host memory with system-scope release, so the
 //           host can poll for it instead of synchronising the stream.
 #include "crc32_kernels.h"
+#include "crc32_layout.h"
 
 namespace rpccrc {
 
