@@ -614,7 +614,8 @@ uint64_t mono_ns() {
 uint32_t scalar_small(const DeviceCtx &c, ScalarCtx &t, const uint8_t *src, uint32_t len) {
   const uint32_t vbytes = 64u << scalar_seg_log2(len);
   if (len) memcpy(t.pin + (vbytes - len), src, len);
-  const uint32_t seq = ++t.seq == 0 ? ++t.seq : t.seq; // 0 is the word's initial value
+  if (++t.seq == 0) t.seq = 1; // 0 is the result word's initial value
+  const uint32_t seq = t.seq;
   if (launch_scalar(t.pin, len, c.scalar_tab, c.tq, t.pres, seq, t.stream) != hipSuccess)
     die("kernel launch", RPCCRC_EIO);
   const volatile uint64_t *res = t.pres;
