@@ -33,6 +33,12 @@ struct ItemsArgs {
   // taken as empty here; launch_big_route computes its CRC afterwards.
   const uint32_t *routed = nullptr;
   uint32_t big_min = 0xFFFFFFFFu;
+  // Tail stealing (QB = 1, DYN launches of host-counted batches): a leased
+  // two-word device counter, zero at launch and reset to zero by the launch's
+  // last workgroup (crc32_rows.h kStealAhead).  nullptr: static rounds only.
+  // steal_s is set by launch_rows.
+  uint32_t *steal = nullptr;
+  uint32_t steal_s = 0;
 };
 
 // ---- big bodies of a ragged batch ----------------------------

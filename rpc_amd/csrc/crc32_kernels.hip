@@ -15,6 +15,7 @@
 //  No MFMA: this is a byte scan.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -175,6 +176,17 @@ __global__ void __launch_bounds__(1024, 4) stream_read_kernel(const uint4 *p, ui
 // ---------------------------------------------------------------------------
 static constexpr int kBlock = 1024;
 
+// Fraction of a launch's rounds dealt from the steal pool (RPCCRC_STEAL_FRAC,
+// 0 disables stealing).
+static double steal_frac() {
+  static const double f = [] {
+    const char *e = getenv("RPCCRC_STEAL_FRAC");
+    const double v = e ? atof(e) : 0.15; // NS: 0.08 / 0.15 / 0.25 -> -3.9 / -4.3 / -3.2 % (r02w)
+    return (v >= 0.0 && v < 1.0) ? v : 0.15;
+  }();
+  return f;
+}
+
 hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream) {
   if (a.n_items == 0) return hipSuccess;
   // The kernel indexes items and tasks in 32 bits: launches of at most
@@ -210,10 +222,21 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // bodies) keep the static one-task-per-wave dealing.
   const uint64_t n_tasks = (QB == 4) ? (a.n_items + 3) / 4 : a.n_items;
   const bool dyn = n_tasks >= 8ull * kDynRound * blocks;
+  // Tail stealing (QB = 1 DYN, host-counted): the last steal_frac of the
+  // rounds go to the device-counter pool, the rest stay static per workgroup.
+  ItemsArgs k = a;
+  k.steal_s = 0;
+  if (dyn && QB == 1 && a.steal != nullptr && a.n_dev == nullptr) {
+    const uint64_t rounds = (n_tasks + kDynRound - 1) / kDynRound;
+    const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac())) / blocks;
+    if (st >= kStealAhead && st * blocks < rounds) k.steal_s = (uint32_t)st;
+  }
+  if (k.steal_s == 0) k.steal = nullptr;
 #define RPCCRC_ROWS(Q, N, R)                                                                      \
   do {                                                                                            \
-    if (dyn) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true>), grid, block, 0, stream, a); \
-    else hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R>), grid, block, 0, stream, a);             \
+    if (dyn && k.steal_s) hipLaunchKernelGGL((crc32_rows_kernel<1, N, R, 0, 1, true, true>), grid, block, 0, stream, k); \
+    else if (dyn) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true>), grid, block, 0, stream, k); \
+    else hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R>), grid, block, 0, stream, k);             \
   } while (0)
   if (QB == 4) {
     if (ragged) {

@@ -442,19 +442,36 @@ struct QuarterInfo {
 // whole 128-B line.
 constexpr uint32_t kDynRound = 32;
 constexpr uint32_t kDynSlots = 4;
-constexpr uint32_t dyn_ctl_words(int QB) { return 1 + 2 * kDynSlots + kDynSlots * kDynRound * (uint32_t)QB; }
+// Tail stealing (DYN with a.steal_s > 0): workgroup vb keeps only its first
+// steal_s local rounds static (global rounds r * blocks + vb); the remaining
+// global rounds form a pool that workgroups claim one round at a time from a
+// device-scope counter (a.steal[0]), so XCDs that stream faster take more of
+// it (per-XCD exit medians differ by up to 20 % with static rounds,
+// profiles/r02/r02t_*).  A claim is issued kStealAhead local rounds ahead, by
+// the wave taking a round's first task, and published into an LDS queue; the
+// workgroup consumes its claimed rounds in publication order, so a claim that
+// returns late is never lost.  A wave never waits (for a queue entry or a
+// ring slot) while it holds an unpublished claim.
+constexpr uint32_t kStealAhead = 2;
+constexpr uint32_t kStealQ = 16;                      // LDS queue ring
+constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
+constexpr uint32_t kStealSpinMax = 1u << 21;          // safety net (~0.1 s): end the wave rather than hang
+constexpr uint32_t dyn_ring_words(int QB) { return 1 + 2 * kDynSlots + kDynSlots * kDynRound * (uint32_t)QB; }
+constexpr uint32_t dyn_ctl_words(int QB) { return dyn_ring_words(QB) + kStealCtlWords; }
 
-template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool DYN = false>
+template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool DYN = false, bool STEAL = false>
 __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   static_assert(!DYN || DEPTH == 1, "DYN: DEPTH = 1");
+  static_assert(!STEAL || (DYN && QB == 1), "stealing: QB = 1 DYN launches");
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
   // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
   // rounds (generation), then the CRC ring (QB CRCs per task).
-  __shared__ uint32_t s_ctl[DYN ? dyn_ctl_words(QB) : 1];
+  __shared__ uint32_t s_ctl[DYN ? (STEAL ? dyn_ctl_words(QB) : dyn_ring_words(QB)) : 1];
   if constexpr (DYN) {
     if (threadIdx.x <= 2 * kDynSlots)
       s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots : 0u;
+    if (STEAL && threadIdx.x < 3 + kStealQ) s_ctl[dyn_ring_words(QB) + threadIdx.x] = 0u; // tail/done/inflight/tags
   }
   // Device-side item counts (split lists, big-body chunks) may be 0: leave
   // before the 155 KiB image copy (block-uniform).
@@ -527,6 +544,91 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     return c;
   };
   auto dyn_task = [&](uint32_t c) -> uint32_t { return (((c / kDynRound) * nblk + vb) * kDynRound) | (c % kDynRound); };
+  // ---- tail stealing (see kStealAhead) ----
+  const uint32_t steal_s = STEAL ? a.steal_s : 0u; // static local rounds per workgroup
+  constexpr bool steal = STEAL;
+  const uint32_t pool_first = steal_s * nblk; // first pool (global) round
+  const uint32_t pool_n = steal ? (n_tasks + kDynRound - 1) / kDynRound - pool_first : 0u;
+  uint32_t *q_ctl = s_ctl + (STEAL ? dyn_ring_words(QB) : 0u);
+  uint32_t *q_tail = q_ctl, *q_done = q_ctl + 1, *q_inflight = q_ctl + 2;
+  uint32_t *q_tag = q_ctl + 3, *q_id = q_ctl + 3 + kStealQ;
+  bool has_claim = false; // wave-uniform: this wave holds an unpublished claim
+  uint32_t claim_v = 0;   // lane 0: the device counter's answer
+  auto lds_ld_acq = [](uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  auto publish = [&]() { // uniform
+    if (!has_claim) return;
+    if (lane == 0) {
+      uint32_t id = claim_v;
+      // keeps the use (and its wait for the atomic) here: hoisted out of a
+      // wait loop it made every pool round's first task wait for its own claim
+      __asm__ volatile("" : "+v"(id));
+      if (id < pool_n) {
+        const uint32_t slot = __hip_atomic_fetch_add(q_tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        q_id[slot % kStealQ] = id;
+        __hip_atomic_store(&q_tag[slot % kStealQ], slot + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        __hip_atomic_store(q_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __hip_atomic_fetch_sub(q_inflight, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    has_claim = false;
+  };
+  // The wave taking local round r's first task claims a pool round for the
+  // workgroup (for use kStealAhead rounds later).
+  auto claim_if_first = [&](uint32_t c) { // uniform
+    if (!steal || c % kDynRound != 0u || c / kDynRound + kStealAhead < steal_s) return;
+    publish(); // at most one claim in flight per wave
+    uint32_t go = 0;
+    if (lane == 0 && lds_ld_acq(q_done) == 0u) {
+      go = 1;
+      __hip_atomic_fetch_add(q_inflight, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // the in-flight count is visible before the device counter moves: a
+      // wave that then sees done && inflight == 0 has seen every claim that
+      // can still return a pool round
+      __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
+      claim_v = __hip_atomic_fetch_add(a.steal, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    has_claim = __builtin_amdgcn_readfirstlane((int)go) != 0;
+  };
+  // Counter index -> global task.  more = false: the workgroup has no work left
+  // (returns n_tasks).  Static rounds as dyn_task; pool rounds from the queue.
+  auto dyn_map = [&](uint32_t c, bool &more) -> uint32_t {
+    const uint32_t r = c / kDynRound;
+    more = true;
+    if (!steal || r < steal_s) return dyn_task(c);
+    const uint32_t q = r - steal_s, k = q % kStealQ;
+    for (uint32_t spin = 0;; ++spin) {
+      uint32_t st = 0, id = 0;
+      if (lane == 0) {
+        if (lds_ld_acq(&q_tag[k]) == q + 1u) {
+          st = 1;
+        } else if (lds_ld_acq(q_done) != 0u && lds_ld_acq(q_inflight) == 0u) {
+          st = (lds_ld_acq(&q_tag[k]) == q + 1u) ? 1u : 2u; // every claim is published: final answer
+        }
+        if (st == 1u) id = q_id[k];
+      }
+      st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
+      if (st == 1u) return ((pool_first + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kDynRound) | (c % kDynRound);
+      if (st == 2u || spin >= kStealSpinMax) break;
+      publish(); // never wait holding a claim
+      __builtin_amdgcn_s_sleep(2);
+    }
+    more = false;
+    return n_tasks;
+  };
+  // Every workgroup passes here once at the end; the last one resets the
+  // device counter for the next launch that leases it.
+  auto steal_exit = [&]() {
+    if (!steal) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(a.steal + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1u == nblk) {
+        __hip_atomic_store(a.steal, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.steal + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
   uint32_t first_c = 0, first_task;
   if constexpr (DYN) {
     first_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)dyn_grab());
@@ -534,7 +636,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   } else {
     first_task = task_of(0);
   }
-  if (first_task >= n_tasks) return;
+  if (first_task >= n_tasks) return; // (never with stealing: local round 0 is static and full)
+  claim_if_first(first_c);
 
   auto synth = [&](uint32_t key, u32x4 (&buf)[4]) {
 #pragma unroll
@@ -634,10 +737,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     // DYN output: CRC of the task with counter index c into the LDS ring; the
     // wave completing a round stores the round's CRCs as one whole line.
-    auto dyn_out = [&](uint32_t c, uint32_t res) {
+    auto dyn_out = [&](uint32_t c, uint32_t tsk, uint32_t res) {
       const uint32_t rnd = c / kDynRound, idx = c % kDynRound, slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots;
       uint32_t old = 0;
+      publish(); // the ring wait below must not hold a claim
       if (lane == 0) {
         // the slot still holds an older round that a slow wave has not finished
         while (__hip_atomic_load(&gen[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rnd)
@@ -646,7 +750,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      const uint32_t base = (rnd * nblk + vb) * kDynRound;
+      // the round's first global task (static rounds: from the local round)
+      const uint32_t base = steal ? tsk & ~(kDynRound - 1u) : (rnd * nblk + vb) * kDynRound;
       const uint32_t cnt = (n_tasks - base < kDynRound) ? n_tasks - base : kDynRound;
       if (old + 1u == cnt) { // this wave completed the round
         const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
@@ -678,7 +783,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     // Horner step and result of a row whose merge is done.
     auto finish = [&](bool valid, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed, uint32_t cidx,
-                      RowMerge m) {
+                      uint32_t tsk, RowMerge m) {
       const bool last = r + 1 == nr;
       // Horner over rows: A_4096(W), or the zlib seed on the item's first row.
       if constexpr ((ABL & kRowsAblLdsSeed) != 0) {
@@ -695,14 +800,14 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (z != 0) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
         if (mode == kModeFinal) res = ~res;
         if constexpr (DYN) {
-          if (valid) dyn_out(cidx, res);
+          if (valid) dyn_out(cidx, tsk, res);
         } else {
           if (valid) park(res);
         }
       }
     };
     auto compute = [&](bool valid, uint32_t hd, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
-                       uint32_t cidx, u32x4 (&buf)[4]) {
+                       uint32_t cidx, uint32_t tsk, u32x4 (&buf)[4]) {
       fix_row(hd, z, nr, r, buf);
       const uint32_t v = quarter_crcs(buf);
       RowMerge m;
@@ -712,7 +817,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         m.crc = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
         m.rwu = W;
       }
-      finish(valid, len, z, nr, r, seed, cidx, m);
+      finish(valid, len, z, nr, r, seed, cidx, tsk, m);
     };
 
     uint32_t c_item = first_task;
@@ -726,24 +831,50 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
     if constexpr (DYN) pend = dyn_grab();
     uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
-    auto succ = [&](bool ok, uint32_t item, uint32_t r, uint32_t nr, uint32_t &s_item, uint32_t &s_r,
-                    bool &s_ok, uint64_t &p0, uint32_t &lp, uint32_t &len, uint32_t &z, uint32_t &snr,
-                    uint32_t &seed) {
+    // more: the wave may still get work (stealing: a task past n inside a
+    // pool round is skipped, not the end).  Invalid rows take one step each.
+    auto succ = [&](bool ok, bool more, uint32_t item, uint32_t r, uint32_t nr, uint32_t &s_item, uint32_t &s_r,
+                    bool &s_ok, bool &s_more, uint64_t &p0, uint32_t &lp, uint32_t &len, uint32_t &z,
+                    uint32_t &snr, uint32_t &seed) {
       const bool adv = r + 1 < nr;
-      if constexpr (DYN) {
+      if constexpr (STEAL) {
         if (adv) {
           s_item = item;
           m_c = c_c;
+          // (`ok && s_item < n`, though implied by ok: written as `ok` it made
+          // the compiler treat the row base as divergent -- a waterfall loop
+          // around every buffer load, ISA)
+          s_ok = ok && s_item < n;
+          s_more = more;
         } else {
-          m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-          s_item = dyn_task(m_c);
-          if (ok && s_item < n) pend = dyn_grab(); // no more grabs once the wave is done
+          s_item = n;
+          s_more = false;
+          if (more) {
+            m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+            claim_if_first(m_c);
+            s_item = dyn_map(m_c, s_more);
+            if (s_more) pend = dyn_grab();
+          }
+          s_ok = s_more && s_item < n;
         }
       } else {
-        s_item = adv ? item : next_task(item);
+        if constexpr (DYN) {
+          if (adv) {
+            s_item = item;
+            m_c = c_c;
+          } else {
+            m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+            s_item = dyn_task(m_c);
+            if (ok && s_item < n) pend = dyn_grab(); // no more grabs once the wave is done
+          }
+        } else {
+          s_item = adv ? item : next_task(item);
+        }
+        s_ok = ok && s_item < n;
+        s_more = s_ok;
       }
-      s_ok = ok && s_item < n;
       meta(s_ok ? s_item : first_task, p0, lp, len, z, snr, seed);
+      if (steal && !s_ok) snr = 1u;
       s_r = adv ? r + 1 : 0u;
     };
     // The unrolled loops have ONE exit, at the bottom: a mid-body break edge
@@ -752,7 +883,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // drain vmcnt before every prefetch (measured: rows fully serialised on
     // half the iterations).  Trailing steps past the wave's last task run on
     // invalid tasks (c_ok false): safe loads, no result parked.
-    bool c_ok = true;
+    bool c_ok = true, c_more = true;
     // Ragged batches only: C2 -1.6 %, while uniform batches (north star
     // +-0.5 %, C4's chunks +0.6 %) keep the plain loop
     // (profiles/r02/r02r_rows_pipeline_ab.txt).
@@ -768,19 +899,20 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
       bool p_ok = false; // no row pending before the first step
-      uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_chain = 0;
+      uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_item = 0, p_chain = 0;
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
         uint32_t m_item, m_lp;
         uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
-        bool m_ok;
-        succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
+        bool m_ok, m_more;
+        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
         fix_row(c_lp, c_z, c_nr, c_r, cb);
         transpose(cb);
         const uint32_t ch = seg_crc(lds, cb, lsel);
         const RowMerge pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
-        finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, pm);
+        finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
+        publish();
         p_ok = c_ok;
         p_len = c_len;
         p_z = c_z;
@@ -788,9 +920,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         p_r = c_r;
         p_seed = c_seed;
         p_c = c_c;
+        p_item = c_item;
         p_chain = ch;
         c_c = m_c;
         c_ok = m_ok;
+        c_more = m_more;
         c_seed = m_seed;
         c_item = m_item;
         c_r = m_r;
@@ -803,7 +937,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       do {
         step(bufA, bufB);
         step(bufB, bufA);
-      } while (p_ok);
+      } while (steal ? (c_more || p_ok) : p_ok);
     } else if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
@@ -811,12 +945,14 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         uint32_t m_item, m_lp;
         uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
-        bool m_ok;
-        succ(c_ok, c_item, c_r, c_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
+        bool m_ok, m_more;
+        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
+        publish();
         c_c = m_c;
         c_ok = m_ok;
+        c_more = m_more;
         c_seed = m_seed;
         c_item = m_item;
         c_r = m_r;
@@ -829,25 +965,25 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       do {
         step(bufA, bufB);
         step(bufB, bufA);
-      } while (c_ok);
+      } while (steal ? c_more : c_ok);
     } else {
       // DEPTH = 2: the next two rows' loads are in flight while one computes.
       u32x4 bufA[4], bufB[4], bufC[4];
       uint32_t n_item, n_lp;
       uint64_t n_p0;
       uint32_t n_r, n_len, n_z, n_nr, n_seed;
-      bool n_ok;
+      bool n_ok, n_more;
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      succ(true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_p0, n_lp, n_len, n_z, n_nr, n_seed);
+      succ(true, true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed);
       issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) {
         uint32_t m_item, m_lp;
         uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
-        bool m_ok;
-        succ(n_ok, n_item, n_r, n_nr, m_item, m_r, m_ok, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
+        bool m_ok, m_more;
+        succ(n_ok, n_more, n_item, n_r, n_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, cb);
+        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, c_item, cb);
         c_ok = n_ok;
         c_seed = n_seed;
         n_seed = m_seed;
@@ -872,6 +1008,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         step(bufC, bufB);
       } while (c_ok);
     }
+    publish();
     flush();
     if constexpr ((ABL & kRowsAblNoStore) != 0)
       if (sink == 0x9E3779B9u) a.out[gw] = sink; // keeps the results live
@@ -1131,6 +1268,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
     }
   }
+  steal_exit();
 }
 
 } // namespace rpccrc

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -163,6 +164,60 @@ struct Lease {
   uint8_t *ptr() const { return static_cast<uint8_t *>(b.p); }
 };
 
+// Two-word device counters for the rows kernel's tail stealing (crc32_rows.h
+// kStealAhead).  A launch leases one; the launch's last workgroup resets it
+// to zero, and the next lessee orders itself after that launch through the
+// slot's event (hipStreamWaitEvent: no host wait).  Slots are 256 B apart.
+class StealPool {
+ public:
+  int acquire(hipStream_t s, uint32_t **p, int *slot) {
+    int k = -1;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (free_.empty())
+        if (const int rc = grow()) return rc;
+      k = free_.back();
+      free_.pop_back();
+    }
+    Slot &x = all_[k];
+    if (x.used) RPCCRC_TRY(hipStreamWaitEvent(s, x.ev, 0));
+    *p = x.p;
+    *slot = k;
+    return RPCCRC_OK;
+  }
+  void release(int k, hipStream_t s) {
+    Slot &x = all_[k];
+    x.used = hipEventRecord(x.ev, s) == hipSuccess;
+    if (!x.used) (void)hipStreamSynchronize(s);
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(k);
+  }
+
+ private:
+  struct Slot {
+    uint32_t *p = nullptr;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  };
+  static constexpr int kChunk = 64;
+  int grow() { // under mu_
+    uint8_t *mem = nullptr;
+    RPCCRC_TRY(hipMalloc(reinterpret_cast<void **>(&mem), kChunk * 256));
+    RPCCRC_TRY(hipMemset(mem, 0, kChunk * 256));
+    for (int i = 0; i < kChunk; ++i) {
+      Slot x;
+      x.p = reinterpret_cast<uint32_t *>(mem + 256 * i);
+      RPCCRC_TRY(hipEventCreateWithFlags(&x.ev, hipEventDisableTiming));
+      free_.push_back((int)all_.size());
+      all_.push_back(x);
+    }
+    return RPCCRC_OK;
+  }
+  std::mutex mu_;
+  std::deque<Slot> all_; // references stay valid as it grows (slots are used outside mu_)
+  std::vector<int> free_;
+};
+
 // A simple free list of T (one borrower at a time, created on demand).
 template <class T>
 class ObjPool {
@@ -236,6 +291,7 @@ struct DeviceCtx {
   BlockPool *pin = nullptr; // pinned staging (keeps <= 256 MiB idle)
   ObjPool<ScalarCtx> *scalar = nullptr;
   ObjPool<HostPipeline> *pipes = nullptr;
+  StealPool *steal = nullptr;
 };
 
 DeviceCtx g_dev[kMaxDevices];
@@ -315,6 +371,7 @@ void init_device(int dev) {
   c.ws = new BlockPool(false, 1ull << 30);
   c.pin = new BlockPool(true, 256ull << 20);
   c.scalar = new ObjPool<ScalarCtx>();
+  c.steal = new StealPool();
   c.pipes = new ObjPool<HostPipeline>();
   c.status = map_hip(e);
 }
@@ -357,9 +414,39 @@ ItemsArgs items_args(const DeviceCtx &c, const uint8_t *base, const uint64_t *of
   return a;
 }
 
+// A tail-stealing counter for a rows launch of n items that deals its rounds
+// dynamically (QB = 1, at least 8 rounds per workgroup; crc32_kernels.hip
+// launch_rows), released after the launch is enqueued.  Used for uniform
+// batches of one-row bodies (north star NS -4.3 %, C3); ragged batches (C2
+// +0.7 %) and the 16 KiB chunks of large bodies (C4 +1.3 %) measured slower
+// with it (profiles/r02/r02w_steal_fraction_ab.txt).
+struct StealLease {
+  StealPool *pool = nullptr;
+  int slot = -1;
+  hipStream_t s = nullptr;
+  uint32_t *p = nullptr;
+  StealLease() = default;
+  StealLease(const StealLease &) = delete;
+  StealLease &operator=(const StealLease &) = delete;
+  ~StealLease() {
+    if (pool) pool->release(slot, s);
+  }
+  int get(const DeviceCtx &c, uint64_t n, int QB, hipStream_t stream) {
+    if (QB != 1 || n < 8ull * 32ull * (uint64_t)max_blocks_for(c)) return RPCCRC_OK;
+    if (const int rc = c.steal->acquire(stream, &p, &slot)) return rc;
+    pool = c.steal;
+    s = stream;
+    return RPCCRC_OK;
+  }
+};
+
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
           uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
-  const ItemsArgs a = items_args(c, base, offsets, lengths, n, stride, len, mode, out);
+  ItemsArgs a = items_args(c, base, offsets, lengths, n, stride, len, mode, out);
+  StealLease sl;
+  if (offsets == nullptr && len <= 4096)
+    if (const int rc = sl.get(c, n, QB, s)) return rc;
+  a.steal = sl.p;
   return map_hip(launch_rows(a, QB, nontemporal(), max_blocks_for(c), s));
 }
 
@@ -418,10 +505,11 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     a.routed = r.routed;
     a.big_min = kBigMin;
   }
-  if (split)
+  if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
-  else
+  } else {
     RPCCRC_TRY(launch_rows(a, 1, nt, mb, s));
+  }
   if (route) RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s));
   return RPCCRC_OK;
 }
