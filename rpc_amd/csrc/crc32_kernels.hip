@@ -222,11 +222,11 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // bodies) keep the static one-task-per-wave dealing.
   const uint64_t n_tasks = (QB == 4) ? (a.n_items + 3) / 4 : a.n_items;
   const bool dyn = n_tasks >= 8ull * kDynRound * blocks;
-  // Tail stealing (QB = 1 DYN, host-counted): the last steal_frac of the
+  // Tail stealing (DYN, host-counted): the last steal_frac of the
   // rounds go to the device-counter pool, the rest stay static per workgroup.
   ItemsArgs k = a;
   k.steal_s = 0;
-  if (dyn && QB == 1 && a.steal != nullptr && a.n_dev == nullptr) {
+  if (dyn && a.steal != nullptr && a.n_dev == nullptr) {
     const uint64_t rounds = (n_tasks + kDynRound - 1) / kDynRound;
     const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac())) / blocks;
     if (st >= kStealAhead && st * blocks < rounds) k.steal_s = (uint32_t)st;
@@ -234,7 +234,7 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   if (k.steal_s == 0) k.steal = nullptr;
 #define RPCCRC_ROWS(Q, N, R)                                                                      \
   do {                                                                                            \
-    if (dyn && k.steal_s) hipLaunchKernelGGL((crc32_rows_kernel<1, N, R, 0, 1, true, true>), grid, block, 0, stream, k); \
+    if (dyn && k.steal_s) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true, true>), grid, block, 0, stream, k); \
     else if (dyn) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true>), grid, block, 0, stream, k); \
     else hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R>), grid, block, 0, stream, k);             \
   } while (0)

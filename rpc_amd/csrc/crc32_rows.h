@@ -463,7 +463,7 @@ template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool
 __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   static_assert(!DYN || DEPTH == 1, "DYN: DEPTH = 1");
-  static_assert(!STEAL || (DYN && QB == 1), "stealing: QB = 1 DYN launches");
+  static_assert(!STEAL || DYN, "stealing: DYN launches");
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
   // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
   // rounds (generation), then the CRC ring (QB CRCs per task).
@@ -1128,11 +1128,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t j0 = 0;
     // DYN output (see QB = 1): the 4 CRCs of group task c into the LDS ring; the
     // wave completing a round stores its (up to) 128 CRCs as two 256-B stores.
-    auto dyn_out4 = [&](uint32_t c, const uint32_t (&v)[4]) {
+    auto dyn_out4 = [&](uint32_t c, uint32_t tsk, const uint32_t (&v)[4]) {
       constexpr uint32_t kW = kDynRound * 4;
       const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots + slot * kW;
       uint32_t old = 0;
+      publish(); // the ring wait below must not hold a claim
       if (lane == 0) {
         while (__hip_atomic_load(&gen[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rnd)
           __builtin_amdgcn_s_sleep(2);
@@ -1141,7 +1142,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      const uint32_t base = (rnd * nblk + vb) * kDynRound; // first group of the round
+      // first group of the round
+      const uint32_t base = steal ? tsk & ~(kDynRound - 1u) : (rnd * nblk + vb) * kDynRound;
       const uint32_t cnt = (ngroups - base < kDynRound) ? (uint32_t)(ngroups - base) : kDynRound;
       if (old + 1u == cnt) {
         const uint32_t ibase = 4 * base;
@@ -1162,7 +1164,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       j0 += ocount / 4u;
       ocount = 0;
     };
-    auto compute = [&](const QuadMeta &qm, bool valid, uint32_t cidx, u32x4 (&buf)[4]) {
+    auto compute = [&](const QuadMeta &qm, bool valid, uint32_t cidx, uint32_t tsk, u32x4 (&buf)[4]) {
       uint32_t zl = 0, zany = 0;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -1191,7 +1193,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
       if (!valid) return; // a trailing step past the wave's last group
       if constexpr (DYN) {
-        dyn_out4(cidx, vals);
+        dyn_out4(cidx, tsk, vals);
       } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) outv = (lane == ocount + (uint32_t)b) ? vals[b] : outv;
@@ -1207,33 +1209,51 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       uint32_t pend = 0;
       if constexpr (DYN) pend = dyn_grab();
       uint32_t c_c = first_c;
-      bool c_ok = true; // the group being computed next is real
+      bool c_ok = true;   // the group being computed next is real
+      bool c_more = true; // stealing: the wave may still get groups (a group past the end is skipped)
       // One exit, at the bottom (see QB = 1): a mid-body break made the
       // compiler drain vmcnt before the next group's loads on every step
       // (ISA: s_waitcnt vmcnt(0) ahead of the offset of the 4th quarter load).
       // Steps past the wave's last group load nothing and store nothing.
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
         uint32_t ng, n_c = 0;
-        if constexpr (DYN) {
-          n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-          ng = dyn_task(n_c);
+        bool ok, more = false;
+        if constexpr (STEAL) {
+          ng = ngroups;
+          if (c_more) {
+            n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+            claim_if_first(n_c);
+            ng = dyn_map(n_c, more);
+            if (more) pend = dyn_grab();
+          }
+          // uniform again after the lane-0 grab (else the compiler carried
+          // `more` as a lane mask and the group index went to VGPRs)
+          more = __builtin_amdgcn_readfirstlane((int)more) != 0;
+          ok = more && ng < ngroups;
         } else {
-          ng = next_task(g);
+          if constexpr (DYN) {
+            n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+            ng = dyn_task(n_c);
+          } else {
+            ng = next_task(g);
+          }
+          ok = c_ok && ng < ngroups;
+          if constexpr (DYN)
+            if (ok) pend = dyn_grab();
         }
-        const bool ok = c_ok && ng < ngroups;
-        if constexpr (DYN)
-          if (ok) pend = dyn_grab();
         const QuadMeta n_qm = issue(ok ? ng : g, ok, safe, nb);
-        compute(c_qm, c_ok, c_c, cb);
+        compute(c_qm, c_ok, c_c, g, cb);
+        publish();
         c_qm = n_qm;
         g = ok ? ng : g;
         c_c = n_c;
         c_ok = ok;
+        c_more = more;
       };
       do {
         step(bufA, bufB);
         step(bufB, bufA);
-      } while (c_ok);
+      } while (steal ? c_more : c_ok);
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
@@ -1243,7 +1263,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         const uint32_t g2 = next_task(gn);
         const bool ok2 = g2 < ngroups;
         const QuadMeta m_qm = issue(ok2 ? g2 : g, ok2, safe, fb);
-        compute(c_qm, true, 0, cb);
+        compute(c_qm, true, 0, g, cb);
         c_qm = n_qm;
         n_qm = m_qm;
         g = gn;
@@ -1256,6 +1276,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (!step(bufC, bufB)) break;
       }
     }
+    publish();
     flush();
     if constexpr ((ABL & kRowsAblTimes) != 0) {
       uint64_t *times = const_cast<uint64_t *>(a.offsets);

@@ -432,7 +432,8 @@ struct StealLease {
     if (pool) pool->release(slot, s);
   }
   int get(const DeviceCtx &c, uint64_t n, int QB, hipStream_t stream) {
-    if (QB != 1 || n < 8ull * 32ull * (uint64_t)max_blocks_for(c)) return RPCCRC_OK;
+    const uint64_t tasks = QB == 4 ? (n + 3) / 4 : n;
+    if (tasks < 8ull * 32ull * (uint64_t)max_blocks_for(c)) return RPCCRC_OK;
     if (const int rc = c.steal->acquire(stream, &p, &slot)) return rc;
     pool = c.steal;
     s = stream;
