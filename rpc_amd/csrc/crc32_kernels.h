@@ -39,6 +39,10 @@ struct ItemsArgs {
   // steal_s is set by launch_rows.
   uint32_t *steal = nullptr;
   uint32_t steal_s = 0;
+  // Words zeroed by workgroup 0 at launch (<= 1024; the contiguous chunk
+  // combine XORs into them afterwards).
+  uint32_t *zero_out = nullptr;
+  uint32_t zero_n = 0;
 };
 
 // ---- big bodies of a ragged batch ----------------------------
@@ -102,6 +106,9 @@ struct CombineArgs {
   uint64_t chunk;               // chunk size in bytes (multiple of 16)
   uint32_t *out;                // splits > 1: zeroed before the launch, blocks XOR their partials in
   uint32_t splits = 1;          // blocks per body (each folds a contiguous run of chunks)
+  // Equal bodies of 4096 * splits power-of-two chunks, 16-B aligned raw, out
+  // zeroed by the rows pass: the contiguous-run kernel (4 chunks per thread).
+  bool contig = false;
   bool inline_bodies = false;   // body table from `bodies` below (n_bodies <= kInlineBodies)
   InlineBodies bodies;
 };

@@ -119,6 +119,44 @@ __global__ void __launch_bounds__(NT) crc32_chunk_combine_kernel(CombineArgs a) 
   }
 }
 
+// Bodies of equal length, a multiple of 4096 power-of-two chunks (C4: 256 MiB
+// in 4 KiB or 16 KiB chunks): a.splits blocks per body, 1024 threads each,
+// thread t of block s folding the CONTIGUOUS run of 4 chunks starting at
+// chunk 4 * (s * 1024 + t) (one 16-B load, three Horner maps), shifted to the
+// body end; the block XORs its threads' runs into out[b], which the rows
+// pass zeroed (ItemsArgs.zero_out).  The combine is bound by LDS lookups (8
+// per map): one block per body (16 CUs for C4) took 21-23 us at 4 KiB
+// chunks, 16 blocks per body spread it over the chip (profiles/r02/r02ab_*).
+__global__ void __launch_bounds__(1024) crc32_chunk_combine_contig_kernel(CombineArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
+  __shared__ uint32_t part[16];
+  const uint64_t b = blockIdx.x / a.splits;
+  const uint32_t s = blockIdx.x % a.splits;
+  const uint32_t t = threadIdx.x;
+  const uint64_t L = a.inline_bodies ? a.bodies.b[b].len : a.lengths[b];
+  const uint64_t first = a.inline_bodies ? a.bodies.b[b].chunk_first : a.chunk_first[b];
+  const uint64_t nch = L / a.chunk;                       // 4096 * splits
+  const uint64_t k0 = 4ull * ((uint64_t)s * 1024u + t); // this thread's first chunk
+  const uint4 v = *reinterpret_cast<const uint4 *>(a.raw + first + k0);
+  {
+    uint4 *dst = reinterpret_cast<uint4 *>(nib);
+#pragma unroll
+    for (uint32_t q = 0; q < kShiftNibWords / 4 / 1024; ++q) dst[q * 1024 + t] = a.shift_nib[q * 1024 + t];
+  }
+  __syncthreads();
+  const uint32_t ks = (uint32_t)__builtin_ctzll(a.chunk); // A_chunk = one nibble map
+  uint32_t acc = nib_apply(nib, ks, nib_apply(nib, ks, nib_apply(nib, ks, v.x) ^ v.y) ^ v.z) ^ v.w;
+  acc = nib_shift(nib, (nch - k0 - 4) * a.chunk, acc);
+  for (int m = 1; m < 64; m <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, m, 64);
+  if ((t & 63u) == 0) part[t >> 6] = acc;
+  __syncthreads();
+  if (t == 0) {
+    for (uint32_t w = 1; w < 16; ++w) acc ^= part[w];
+    if (s == 0) acc ^= ~nib_shift(nib, L, 0xFFFFFFFFu);
+    atomicXor(a.out + b, acc);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Synthetic data: counter-based splitmix64 words (same stream as
 // oracle_splitmix_fill): word k = mix64(seed + (k+1) * golden), little-endian.
@@ -260,7 +298,9 @@ hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream) {
   const uint64_t blocks = a.n_bodies * a.splits;
   if (a.splits == 0 || blocks >= (1ull << 31)) return hipErrorInvalidValue;
   if (a.inline_bodies && a.n_bodies > kInlineBodies) return hipErrorInvalidValue;
-  if (a.splits == 1)
+  if (a.contig)
+    hipLaunchKernelGGL(crc32_chunk_combine_contig_kernel, dim3((unsigned)blocks), dim3(1024), 0, stream, a);
+  else if (a.splits == 1)
     hipLaunchKernelGGL(crc32_chunk_combine_kernel<1024>, dim3((unsigned)blocks), dim3(1024), 0, stream, a);
   else
     hipLaunchKernelGGL(crc32_chunk_combine_kernel<256>, dim3((unsigned)blocks), dim3(256), 0, stream, a);

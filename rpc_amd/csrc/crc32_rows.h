@@ -475,6 +475,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   }
   // Device-side item counts (split lists, big-body chunks) may be 0: leave
   // before the 155 KiB image copy (block-uniform).
+  if (blockIdx.x == 0 && threadIdx.x < a.zero_n) a.zero_out[threadIdx.x] = 0u;
   if (a.n_dev != nullptr && ld_const(a.n_dev, 0) == 0) return;
   uint64_t t_entry = 0, t_image = 0;
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();

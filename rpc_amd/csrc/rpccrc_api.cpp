@@ -580,9 +580,17 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     lens_or |= h_lengths[i];
     if (i + 1 < n && h_offsets[i + 1] != h_offsets[i] + h_lengths[i]) contiguous = false;
   }
+  bool equal = true;
+  for (uint64_t i = 1; i < n && equal; ++i) equal = h_lengths[i] == h_lengths[0];
   if (chunk == 0) {
     chunk = g_large_chunk;
-    if (contiguous && lens_or % chunk != 0 && !g_large_chunk_env)
+    // Back-to-back equal bodies of a multiple of 16 MiB: one-row 4 KiB chunks,
+    // dealt with tail stealing and folded by the contiguous-run combine
+    // (C4 640 -> 618 us, profiles/r02/r02ac_*).
+    if (contiguous && equal && n <= 1024 && h_lengths[0] != 0 && h_lengths[0] % (4096ull * 4096ull) == 0 &&
+        h_lengths[0] / 4096 <= 16ull * 4096ull && !g_large_chunk_env)
+      chunk = 4096;
+    else if (contiguous && lens_or % chunk != 0 && !g_large_chunk_env)
       for (uint64_t cand : {8192ull, 4096ull})
         if (lens_or % cand == 0) {
           chunk = cand;
@@ -600,6 +608,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     bd = reinterpret_cast<BodyDesc *>(stage.ptr());
   }
   bool multiple = true;
+  uint64_t min_nch = ~0ull;
   for (uint64_t i = 0; i < n; ++i) {
     bd[i].off = h_offsets[i];
     bd[i].len = h_lengths[i];
@@ -607,6 +616,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     const uint64_t nch = (h_lengths[i] + chunk - 1) / chunk;
     total += nch;
     max_nch = std::max(max_nch, nch);
+    min_nch = std::min(min_nch, nch);
     if (!pow2 && h_lengths[i] % chunk != 0) multiple = false;
   }
   if (pow2) multiple = lens_or % chunk == 0;
@@ -620,6 +630,11 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     splits = std::max<uint64_t>(1, std::min<uint64_t>(splits, (1ull << 20) / n));
   }
   const bool fast = contiguous && multiple && splits == 1;
+  // Equal bodies of 4096 * S power-of-two chunks (S <= 16) on the fast path:
+  // the contiguous-run combine with S blocks per body (the rows pass zeroes out).
+  const uint64_t cs = max_nch / 4096;
+  const bool contig = fast && min_nch == max_nch && max_nch % 4096 == 0 && cs >= 1 && cs <= 16 &&
+                      (chunk & (chunk - 1)) == 0 && n <= 1024;
   const size_t ws_bytes = fast ? total * 4 + 64 : n * sizeof(BodyDesc) + n * 16 + total * (8 + 4 + 4) + 64;
   Lease wsl;
   if (const int rc = wsl.get(c.ws, ws_bytes, s)) return rc;
@@ -627,9 +642,16 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   uint32_t *d_raw = reinterpret_cast<uint32_t *>(ws);
   uint64_t *d_lens = nullptr, *d_firsts = nullptr;
   if (fast) {
-    RPCCRC_TRY(launch_rows(items_args(c, d_base + h_offsets[0], nullptr, nullptr, total, chunk, (uint32_t)chunk,
-                                      kModeRaw, d_raw),
-                           1, nontemporal(), max_blocks_for(c), s));
+    ItemsArgs k = items_args(c, d_base + h_offsets[0], nullptr, nullptr, total, chunk, (uint32_t)chunk, kModeRaw, d_raw);
+    StealLease sl; // one-row chunks deal like the north star (items())
+    if (chunk <= 4096)
+      if (const int rc = sl.get(c, total, 1, s)) return rc;
+    k.steal = sl.p;
+    if (contig) {
+      k.zero_out = d_out;
+      k.zero_n = (uint32_t)n;
+    }
+    RPCCRC_TRY(launch_rows(k, 1, nontemporal(), max_blocks_for(c), s));
   } else {
     BodyDesc *d_bodies = reinterpret_cast<BodyDesc *>(ws);
     d_lens = reinterpret_cast<uint64_t *>(ws + n * sizeof(BodyDesc));
@@ -659,6 +681,10 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   ca.chunk = chunk;
   ca.out = d_out;
   ca.splits = (uint32_t)splits;
+  if (contig) {
+    ca.contig = true;
+    ca.splits = (uint32_t)cs;
+  }
   ca.inline_bodies = inl;
   if (inl) ca.bodies = ib;
   return map_hip(launch_chunk_combine(ca, s));

@@ -327,6 +327,20 @@ def test_device_large_contiguous(chunk, lens):
         assert got2.tolist() == [oracle.crc32(host2[o:o + L]) for o, L in zip(offs2, lens2)]
 
 
+@pytest.mark.parametrize("chunk,blen,nb,gap", [
+    (256, 4 << 20, 3, 0),    # 16Ki chunks per body: contiguous-run combine, M = 16
+    (256, 8 << 20, 2, 0),    # M = 32
+    (1024, 64 << 20, 2, 0),  # M = 64 (C4's shape at 4 KiB chunks: 64Ki chunks per body)
+    (256, 4 << 20, 3, 3),    # gaps between bodies: chunk-table path, same combine when aligned
+])
+def test_device_large_equal_bodies_combine(chunk, blen, nb, gap):
+    """Equal bodies of 1024 * M power-of-two chunks take crc32_chunk_combine_contig_kernel."""
+    offs = [5 + i * (blen + gap) for i in range(nb)]
+    host = oracle.splitmix_bytes(offs[-1] + blen + 16, 777 + blen + gap)
+    got = u32(rpc_amd.device_large(to_dev(host), offs, [blen] * nb, chunk=chunk))
+    assert got.tolist() == [oracle.crc32(host[o:o + blen]) for o in offs]
+
+
 def test_nontemporal_option_same_result():
     host = oracle.splitmix_bytes(4096 * 500, 8)
     base = to_dev(host)
