@@ -92,7 +92,7 @@ for s in $STEPS; do
                python3 bench.py --config c4 --chunk-kib $k --steps 10 --warmup 3 --prewarm-s 0.2 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
            done ;;
     packed) run packed 600 python tools/probe.py --mode packed --rounds 3 --reps 5 ;;
-    bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive --steps 5 ;;
+    bench_c4) run bench_c4 600 python bench.py --config c4 --no-cpu-baseline --no-host-inclusive ;;
     counters) run counters 120 rocprofv3 -L ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
