@@ -167,20 +167,24 @@ struct Lease {
 // Two-word device counters for the rows kernel's tail stealing (crc32_rows.h
 // kStealAhead).  A launch leases one; the launch's last workgroup resets it
 // to zero, and the next lessee orders itself after that launch through the
-// slot's event (hipStreamWaitEvent: no host wait).  Slots are 256 B apart.
+// slot's event (hipStreamWaitEvent: no host wait).  Slots are 256 B apart and
+// leased least-recently-used first, so back-to-back launches find their
+// slot's last use finished and skip the wait: a wait per launch put ~5 us
+// between back-to-back C1 kernels (profiles/r02/r02af_c1_kernel_stats.csv
+// vs r02af_bench_c1.log).
 class StealPool {
  public:
   int acquire(hipStream_t s, uint32_t **p, int *slot) {
     int k = -1;
     {
       std::lock_guard<std::mutex> g(mu_);
-      if (free_.empty())
+      if (free_.size() < kMinFree)
         if (const int rc = grow()) return rc;
-      k = free_.back();
-      free_.pop_back();
+      k = free_.front();
+      free_.pop_front();
     }
     Slot &x = all_[k];
-    if (x.used) RPCCRC_TRY(hipStreamWaitEvent(s, x.ev, 0));
+    if (x.used && hipEventQuery(x.ev) != hipSuccess) RPCCRC_TRY(hipStreamWaitEvent(s, x.ev, 0));
     *p = x.p;
     *slot = k;
     return RPCCRC_OK;
@@ -200,6 +204,7 @@ class StealPool {
     bool used = false;
   };
   static constexpr int kChunk = 64;
+  static constexpr size_t kMinFree = 16; // grow early: a slot rests >= 16 leases before reuse
   int grow() { // under mu_
     uint8_t *mem = nullptr;
     RPCCRC_TRY(hipMalloc(reinterpret_cast<void **>(&mem), kChunk * 256));
@@ -215,7 +220,7 @@ class StealPool {
   }
   std::mutex mu_;
   std::deque<Slot> all_; // references stay valid as it grows (slots are used outside mu_)
-  std::vector<int> free_;
+  std::deque<int> free_;  // FIFO: least recently used first
 };
 
 // A simple free list of T (one borrower at a time, created on demand).
