@@ -341,6 +341,27 @@ def test_device_large_equal_bodies_combine(chunk, blen, nb, gap):
     assert got.tolist() == [oracle.crc32(host[o:o + blen]) for o in offs]
 
 
+def test_tail_stealing_back_to_back_launches():
+    """Uniform one-row batches deal their last rounds from a leased device counter
+    that each launch's last workgroup resets (crc32_rows.h kStealAhead).  70
+    launches back to back on one stream cycle through the counter slots (64 per
+    pool chunk), two streams interleave, and every launch must produce every CRC."""
+    n, L = 65536, 4096  # the smallest batch that deals dynamically on 256 CUs
+    host = oracle.splitmix_bytes(n * L, 0x57EA1)
+    base = to_dev(host)
+    ref = u32(rpc_amd.device_uniform(base, n, L))
+    assert np.array_equal(ref, oracle.crc32_uniform_mt(host, n, L))
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for k in range(70):
+        st = s1 if k % 3 else s2
+        with torch.cuda.stream(st):
+            outs.append(rpc_amd.device_uniform(base, n, L, stream=st))
+    torch.cuda.synchronize()
+    for k, o in enumerate(outs):
+        assert np.array_equal(u32(o), ref), k
+
+
 def test_nontemporal_option_same_result():
     host = oracle.splitmix_bytes(4096 * 500, 8)
     base = to_dev(host)
