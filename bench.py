@@ -82,6 +82,11 @@ def parse():
     p.add_argument("--no-scalar-latency", action="store_true")
     p.add_argument("--no-live-traffic", action="store_true",
                    help="skip the two rocprofv3 PMC child passes (roofline.traffic from profiles/traffic.json)")
+    p.add_argument("--step-events", type=int, default=0,
+                   help="0: events only around the K timed steps (value, mean launch time); the per-launch "
+                        "median then comes from a second K-step pass with an event after every step. 1: per-step "
+                        "events in the timed pass itself (each event is a marker packet between launches: "
+                        "+4 us per C1 step, profiles/r02/r02aj_step_events_ab.txt)")
     p.add_argument("--prewarm-s", type=float, default=0.5,
                    help="untimed steps before the W warmup steps until this much time has passed: the GPU "
                         "clock ramps over the first ~20 launches of sustained load (DESIGN.md 5)")
@@ -452,22 +457,43 @@ def main():
     if dist:
         barrier(dist, device)
     torch.cuda.synchronize()
-    # One event per step boundary on the kernel's stream: per-launch durations
-    # (mean = roofline.achieved, median reported beside it).
+    # Events on the kernel's stream around the K steps (mean launch time =
+    # roofline.achieved).  An event between launches is a marker packet that
+    # delays the next launch, so per-step events (for the median)
+    # are taken in a second pass below unless --step-events 1.
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     evs[0].record(stream)
     for k in range(args.steps):
         w.step()
-        evs[k + 1].record(stream)
+        if args.step_events or k + 1 == args.steps:
+            evs[k + 1].record(stream)
     torch.cuda.synchronize()
     if dist:
         barrier(dist, device)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    step_s = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(args.steps)]
+    if args.step_events:
+        step_s = [evs[k].elapsed_time(evs[k + 1]) / 1e3 for k in range(args.steps)]
+    else:
+        step_s = [evs[0].elapsed_time(evs[args.steps]) / 1e3 / args.steps] * args.steps
     kernel_s = sum(step_s) / args.steps  # avg launch duration on the kernel's stream
     median_s = float(np.median(step_s))
+    median_src = "timed pass, an event after every step" if args.step_events else None
+    if not args.step_events:
+        mev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        # The clock drops during the sync above and takes ~20 launches to ramp
+        # back (a median over 5 re-warm launches read 16 % slow): ~0.3 s of
+        # launches first, enqueued back to back with the measured ones.
+        for _ in range(max(args.warmup, int(0.3 / max(kernel_s, 1e-6)))):
+            w.step()
+        mev[0].record(stream)
+        for k in range(args.steps):
+            w.step()
+            mev[k + 1].record(stream)
+        torch.cuda.synchronize()
+        median_s = float(np.median([mev[k].elapsed_time(mev[k + 1]) / 1e3 for k in range(args.steps)]))
+        median_src = "second K-step pass with an event after every step (each adds a marker between launches)"
     tmax = max_over_ranks(dist, wall, device) if dist else wall
     total_bytes = sum_over_ranks(dist, w.total, device) if dist else w.total
 
@@ -538,6 +564,7 @@ def main():
                            "large": "crc32_rows_kernel (+chunk combine)"}[w.kind],
                 "avg_launch_us": round(kernel_s * 1e6, 2),
                 "median_launch_us": round(median_s * 1e6, 2),
+                "median_source": median_src,
                 "algo_bytes_per_launch": w.algo_bytes,
                 # the same achieved rate against a streaming read
                 # of the same buffer on the same GPU (non-temporal, the rows
