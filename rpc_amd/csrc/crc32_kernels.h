@@ -119,8 +119,14 @@ constexpr uint64_t kMaxLaunchItems = 1ull << 30;
 
 // QB = 1: rows of 4 KiB of one item (any length); QB = 4: four items per row,
 // each with len + ((-(end address)) & 15) <= 1024.
-hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream);
-hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream);
+// steal_done: the steal-counter slot's event.  A launch that deals from the
+// counter (a.steal) records it as the kernel's own completion signal
+// (hipExtLaunchKernel stopEvent: no marker packet between back-to-back
+// launches) and sets *steal_recorded.
+hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream,
+                       hipEvent_t steal_done = nullptr, bool *steal_recorded = nullptr);
+// done: optional event recorded as the combine kernel's completion signal.
+hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream, hipEvent_t done = nullptr);
 
 // Packed ragged batches (crc32_packed.h): 1 KiB chunks of consecutive bodies,
 // four per row, balanced by chunk count; n < 2^32 - 1.  ws must hold

@@ -13,6 +13,7 @@
 //  * splitmix_fill_kernel / stream_read_kernel: synthetic data and the
 //    achievable-HBM-read probe used by bench.py.
 //  No MFMA: this is a byte scan.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -225,7 +226,8 @@ static double steal_frac() {
   return f;
 }
 
-hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream) {
+hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream, hipEvent_t steal_done,
+                       bool *steal_recorded) {
   if (a.n_items == 0) return hipSuccess;
   // The kernel indexes items and tasks in 32 bits: launches of at most
   // kMaxLaunchItems (a multiple of 4: QB = 4 groups never straddle launches).
@@ -241,7 +243,7 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
         b.base += s0 * a.stride;
       }
       b.out += s0;
-      const hipError_t e = launch_rows(b, QB, nt, max_blocks, stream);
+      const hipError_t e = launch_rows(b, QB, nt, max_blocks, stream, steal_done, steal_recorded);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -272,7 +274,15 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   if (k.steal_s == 0) k.steal = nullptr;
 #define RPCCRC_ROWS(Q, N, R)                                                                      \
   do {                                                                                            \
-    if (dyn && k.steal_s) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true, true>), grid, block, 0, stream, k); \
+    if (dyn && k.steal_s) {                                                                       \
+      if (steal_done) {                                                                           \
+        hipExtLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true, true>), grid, block, 0, stream, nullptr, \
+                              steal_done, 0, k);                                                  \
+        if (steal_recorded) *steal_recorded = true;                                               \
+      } else {                                                                                    \
+        hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true, true>), grid, block, 0, stream, k); \
+      }                                                                                           \
+    }                                                                                             \
     else if (dyn) hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R, 0, 1, true>), grid, block, 0, stream, k); \
     else hipLaunchKernelGGL((crc32_rows_kernel<Q, N, R>), grid, block, 0, stream, k);             \
   } while (0)
@@ -293,17 +303,20 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   return hipGetLastError();
 }
 
-hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream) {
-  if (a.n_bodies == 0) return hipSuccess;
+hipError_t launch_chunk_combine(const CombineArgs &a, hipStream_t stream, hipEvent_t done) {
+  if (a.n_bodies == 0) return done ? hipEventRecord(done, stream) : hipSuccess;
   const uint64_t blocks = a.n_bodies * a.splits;
   if (a.splits == 0 || blocks >= (1ull << 31)) return hipErrorInvalidValue;
   if (a.inline_bodies && a.n_bodies > kInlineBodies) return hipErrorInvalidValue;
   if (a.contig)
-    hipLaunchKernelGGL(crc32_chunk_combine_contig_kernel, dim3((unsigned)blocks), dim3(1024), 0, stream, a);
+    hipExtLaunchKernelGGL(crc32_chunk_combine_contig_kernel, dim3((unsigned)blocks), dim3(1024), 0, stream, nullptr,
+                          done, 0, a);
   else if (a.splits == 1)
-    hipLaunchKernelGGL(crc32_chunk_combine_kernel<1024>, dim3((unsigned)blocks), dim3(1024), 0, stream, a);
+    hipExtLaunchKernelGGL(crc32_chunk_combine_kernel<1024>, dim3((unsigned)blocks), dim3(1024), 0, stream, nullptr,
+                          done, 0, a);
   else
-    hipLaunchKernelGGL(crc32_chunk_combine_kernel<256>, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+    hipExtLaunchKernelGGL(crc32_chunk_combine_kernel<256>, dim3((unsigned)blocks), dim3(256), 0, stream, nullptr,
+                          done, 0, a);
   return hipGetLastError();
 }
 

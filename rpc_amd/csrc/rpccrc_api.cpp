@@ -109,9 +109,11 @@ class BlockPool {
   }
 
   // Returns the block after the call has enqueued its last use on stream s.
-  void release(Block &b, hipStream_t s) {
+  // recorded: the call's last kernel already recorded b.ev as its completion
+  // signal (hipExtLaunchKernel stopEvent), so no marker packet is needed here.
+  void release(Block &b, hipStream_t s, bool recorded = false) {
     if (!b.p) return;
-    b.used = hipEventRecord(b.ev, s) == hipSuccess;
+    b.used = recorded || hipEventRecord(b.ev, s) == hipSuccess;
     if (!b.used) (void)hipStreamSynchronize(s); // no event: make the block idle now
     std::vector<Block> evict;
     {
@@ -150,12 +152,16 @@ struct Lease {
   BlockPool *pool = nullptr;
   Block b;
   hipStream_t s = nullptr;
+  bool recorded = false; // the call's last launch recorded b.ev (done_event())
   Lease() = default;
   Lease(const Lease &) = delete;
   Lease &operator=(const Lease &) = delete;
   ~Lease() {
-    if (pool) pool->release(b, s);
+    if (pool) pool->release(b, s, recorded);
   }
+  // The block's event, for the call's LAST launch on s to record as its own
+  // completion (then set `recorded`).
+  hipEvent_t done_event() const { return b.ev; }
   int get(BlockPool *p, size_t bytes, hipStream_t stream) {
     pool = p;
     s = stream;
@@ -174,7 +180,7 @@ struct Lease {
 // vs r02af_bench_c1.log).
 class StealPool {
  public:
-  int acquire(hipStream_t s, uint32_t **p, int *slot) {
+  int acquire(hipStream_t s, uint32_t **p, int *slot, hipEvent_t *ev) {
     int k = -1;
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -187,12 +193,20 @@ class StealPool {
     if (x.used && hipEventQuery(x.ev) != hipSuccess) RPCCRC_TRY(hipStreamWaitEvent(s, x.ev, 0));
     *p = x.p;
     *slot = k;
+    *ev = x.ev;
     return RPCCRC_OK;
   }
-  void release(int k, hipStream_t s) {
+  // recorded: the launch recorded the slot's event as its completion signal
+  // (launch_rows steal_done).  Otherwise the slot may have been used by a
+  // launch without it (ext_event() off): record it here, a marker packet.
+  void release(int k, hipStream_t s, bool recorded, bool dealt) {
     Slot &x = all_[k];
-    x.used = hipEventRecord(x.ev, s) == hipSuccess;
-    if (!x.used) (void)hipStreamSynchronize(s);
+    if (recorded) {
+      x.used = true;
+    } else if (dealt) {
+      x.used = hipEventRecord(x.ev, s) == hipSuccess;
+      if (!x.used) (void)hipStreamSynchronize(s);
+    } // else the launch did not touch the slot: its last use (and event) stand
     std::lock_guard<std::mutex> g(mu_);
     free_.push_back(k);
   }
@@ -425,25 +439,40 @@ ItemsArgs items_args(const DeviceCtx &c, const uint8_t *base, const uint64_t *of
 // batches of one-row bodies (north star NS -4.3 %, C3); ragged batches (C2
 // +0.7 %) and the 16 KiB chunks of large bodies (C4 +1.3 %) measured slower
 // with it (profiles/r02/r02w_steal_fraction_ab.txt).
+// The slot's event is bound to the kernel's completion (launch_rows
+// steal_done, hipExtLaunchKernel): a separate hipEventRecord after each launch
+// is a marker packet between back-to-back kernels (+4 us per C1 step with
+// per-step events, profiles/r02/r02aj_step_events_ab.txt).
+// RPCCRC_STEAL_EXT_EVENT=0 records it separately (A/B only).
+bool steal_ext_event() {
+  static const bool v = [] {
+    const char *e = getenv("RPCCRC_STEAL_EXT_EVENT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 struct StealLease {
   StealPool *pool = nullptr;
   int slot = -1;
   hipStream_t s = nullptr;
   uint32_t *p = nullptr;
+  hipEvent_t ev = nullptr;
+  bool recorded = false; // the launch recorded ev itself
   StealLease() = default;
   StealLease(const StealLease &) = delete;
   StealLease &operator=(const StealLease &) = delete;
   ~StealLease() {
-    if (pool) pool->release(slot, s);
+    if (pool) pool->release(slot, s, recorded, !steal_ext_event());
   }
   int get(const DeviceCtx &c, uint64_t n, int QB, hipStream_t stream) {
     const uint64_t tasks = QB == 4 ? (n + 3) / 4 : n;
     if (tasks < 8ull * 32ull * (uint64_t)max_blocks_for(c)) return RPCCRC_OK;
-    if (const int rc = c.steal->acquire(stream, &p, &slot)) return rc;
+    if (const int rc = c.steal->acquire(stream, &p, &slot, &ev)) return rc;
     pool = c.steal;
     s = stream;
     return RPCCRC_OK;
   }
+  hipEvent_t done_event() const { return steal_ext_event() ? ev : nullptr; }
 };
 
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
@@ -453,7 +482,7 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
   if (offsets == nullptr && len <= 4096)
     if (const int rc = sl.get(c, n, QB, s)) return rc;
   a.steal = sl.p;
-  return map_hip(launch_rows(a, QB, nontemporal(), max_blocks_for(c), s));
+  return map_hip(launch_rows(a, QB, nontemporal(), max_blocks_for(c), s, sl.done_event(), &sl.recorded));
 }
 
 // A ragged batch on the device.
@@ -656,7 +685,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
       k.zero_out = d_out;
       k.zero_n = (uint32_t)n;
     }
-    RPCCRC_TRY(launch_rows(k, 1, nontemporal(), max_blocks_for(c), s));
+    RPCCRC_TRY(launch_rows(k, 1, nontemporal(), max_blocks_for(c), s, sl.done_event(), &sl.recorded));
   } else {
     BodyDesc *d_bodies = reinterpret_cast<BodyDesc *>(ws);
     d_lens = reinterpret_cast<uint64_t *>(ws + n * sizeof(BodyDesc));
@@ -692,6 +721,11 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   }
   ca.inline_bodies = inl;
   if (inl) ca.bodies = ib;
+  if (steal_ext_event()) {
+    const hipError_t e = launch_chunk_combine(ca, s, wsl.done_event());
+    wsl.recorded = e == hipSuccess;
+    return map_hip(e);
+  }
   return map_hip(launch_chunk_combine(ca, s));
 }
 
