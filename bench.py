@@ -300,6 +300,60 @@ def scalar_latency_probe():
     return r
 
 
+def frames_lifted_probe(device, n=1024, reps=5, seed=0x5EED0007):
+    """SURVEY.md 8f row 3 (large-body framing): n rpc.h frames back to back in
+    HBM, bodies log-uniform 1 B - 64 MiB (MAX_BODY_LEN lifted, RPC_FRAMES_LIFT_CAP),
+    stamped and then verified on the device.  Bodies >= 256 KiB take the
+    on-device chunk route.  Checks: every frame verifies OK after
+    the stamp, and one byte flipped inside the largest body is flagged BAD_CRC
+    (the CRCs themselves are checked against the oracle by
+    tests/test_frames.py::test_frames_lifted_cap_large_bodies)."""
+    lens = _loguniform_lengths(n, seed, lo=1, hi=64 << 20).astype(np.uint64)
+    sizes = lens + np.uint64(12)
+    offs = np.concatenate([[0], np.cumsum(sizes[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(offs[-1] + sizes[-1])
+    buf = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=device)
+    rpc_amd.fill_random(buf, seed)
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
+    d_lens = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(device)
+    stream = torch.cuda.current_stream()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / reps
+
+    st = {}
+    t_stamp = timed(lambda: st.__setitem__("v", rpc_amd.frames_stamp(buf, d_offs, d_lens, lift_cap=True,
+                                                                      stream_bytes=total)))
+    stamped = bool((st["v"] == rpc_amd.FRAME_OK).all().item())
+    vr = {}
+    t_verify = timed(lambda: vr.__setitem__("v", rpc_amd.frames_verify(buf, d_offs, lift_cap=True,
+                                                                       stream_bytes=total)[0]))
+    all_ok = bool((vr["v"] == rpc_amd.FRAME_OK).all().item())
+    big = int(np.argmax(lens))
+    pos = int(offs[big]) + 12 + int(lens[big]) // 2
+    buf[pos] ^= 0x5A
+    v2, _ = rpc_amd.frames_verify(buf, d_offs, lift_cap=True, stream_bytes=total)
+    v2 = v2.cpu().numpy()
+    buf[pos] ^= 0x5A
+    flagged = bool(v2[big] == rpc_amd.FRAME_BAD_CRC and (np.delete(v2, big) == rpc_amd.FRAME_OK).all())
+    body = int(lens.sum())
+    del buf
+    return {"frames": n, "bodies": "log-uniform 1 B - 64 MiB (LIFT_CAP)", "body_bytes": body,
+            "routed_bodies_ge_256KiB": int((lens >= (256 << 10)).sum()),
+            "verify_us": round(t_verify * 1e6, 1), "verify_GiBps": round(body / t_verify / GiB, 1),
+            "verify_frames_per_s": round(n / t_verify, 1),
+            "stamp_us": round(t_stamp * 1e6, 1), "stamp_GiBps": round(body / t_stamp / GiB, 1),
+            "all_stamped": stamped, "all_ok_after_stamp": all_ok, "corrupted_frame_flagged": flagged}
+
+
 def stream_read_probe(w: Workload, reps=10):
     """Achievable HBM read rate on the same buffer: a pure streaming read with
     coalesced 16-B lanes, non-temporal (the CRC kernel's load shape) and
@@ -508,6 +562,9 @@ def main():
             if w.kind == "uniform":
                 log("receive ring")
                 extra["rx_ring"] = rx_ring_probe()
+        if w.name == "ns" and not args.no_host_inclusive:
+            log("lifted-cap frames (1 B - 64 MiB bodies)")
+            extra["frames_lifted"] = frames_lifted_probe(device)
         if not args.no_scalar_latency and not args.no_host_inclusive:
             log("scalar latency")
             extra["scalar_latency"] = scalar_latency_probe()
