@@ -46,3 +46,45 @@ def sum_over_ranks(dist, value: int, device=None) -> int:
     t = torch.tensor([value], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+# ---- one large body across GPUs (SURVEY.md 8e, optional for C4) -------------
+# A body too large for one GPU's share of the work is cut into contiguous byte
+# ranges, one per rank; each rank CRCs its range on its own GPU
+# (rpc_crc32_device_large), and the ONE exchange step is an all-gather of the
+# 4-B partials and their lengths, folded in body order with zlib crc32_combine
+# semantics: crc(A || B) = crc32_combine(crc(A), crc(B), len(B)).
+
+def large_body_range(length: int, rank: int, world: int, align: int = 4096) -> tuple[int, int]:
+    """[lo, hi) bytes of one body for `rank`: balanced, cut at multiples of
+    `align` (so every range but the last is a whole number of rows)."""
+    if align <= 0:
+        raise ValueError("align must be positive")
+    units = (length + align - 1) // align
+    lo, hi = shard_range(units, rank, world)
+    return min(lo * align, length), min(hi * align, length)
+
+
+def fold_partials(parts, combine) -> int:
+    """CRC of the concatenation of ranges whose (crc, length) pairs are `parts`,
+    in body order.  `combine` is zlib's crc32_combine (rpc_crc32_combine)."""
+    crc = 0  # CRC of the empty prefix; combine(0, c, n) == c
+    for c, n in parts:
+        crc = combine(crc, int(c) & 0xFFFFFFFF, int(n))
+    return crc
+
+
+def sharded_large_crc(dist, local_crc: int, local_len: int, device=None, combine=None) -> int:
+    """Every rank passes the CRC of its range of the body (ranges in rank
+    order); returns the whole body's CRC on every rank.  One all_gather of
+    (crc, len) per rank -- RCCL over xGMI with the "nccl" backend."""
+    import torch
+
+    if combine is None:
+        import rpc_amd
+
+        combine = rpc_amd.crc32_combine
+    mine = torch.tensor([int(local_crc) & 0xFFFFFFFF, int(local_len)], dtype=torch.int64, device=device)
+    parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, mine)
+    return fold_partials([(int(p[0]), int(p[1])) for p in parts], combine)

@@ -11,7 +11,8 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from rpc_amd.shard import max_over_ranks, rank_seed, shard_range, sum_over_ranks, barrier
+from rpc_amd.shard import (barrier, fold_partials, large_body_range, max_over_ranks, rank_seed, shard_range,
+                           sharded_large_crc, sum_over_ranks)
 
 
 def _free_port():
@@ -121,3 +122,77 @@ def test_gloo_world2_hip_shards_match_oracle():
         assert p.exitcode == 0
     assert n == 30011 and bad == 0
     assert "gfx950" in info
+
+
+# ---- one large body across ranks (optional for C4) ---------------
+
+def test_large_body_range_and_fold():
+    import zlib
+
+    import rpc_amd
+    from oracle import oracle
+    data = oracle.splitmix_bytes(100_003, 9)
+    for world in [1, 2, 3, 8]:
+        for align in [16, 4096, 65536]:
+            rs = [large_body_range(len(data), r, world, align) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == len(data)
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert all(lo % align == 0 for lo, _ in rs)
+            parts = [(oracle.crc32(data[a:b]), b - a) for a, b in rs]
+            assert fold_partials(parts, rpc_amd.crc32_combine) == zlib.crc32(data)
+    assert fold_partials([], rpc_amd.crc32_combine) == 0
+
+
+def _large_worker(rank, world, port, q, on_gpu):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+
+        import rpc_amd
+        from oracle import oracle
+        length = (24 << 20) + 12345  # not a multiple of the range alignment
+        lo, hi = large_body_range(length, rank, world)
+        if on_gpu:
+            torch.cuda.set_device(0)
+            x = torch.empty((length + 7) // 8 * 8, dtype=torch.uint8, device="cuda:0")
+            rpc_amd.fill_random(x, 0x5EED0006)  # every rank sees the same logical body
+            mine = int(rpc_amd.device_large(x, [lo], [hi - lo]).cpu().numpy().view(np.uint32)[0])
+            body = x[:length].cpu().numpy()
+        else:  # CPU: the oracle stands in for the device CRC of the rank's range
+            body = oracle.splitmix_bytes(length, 0x5EED0006)
+            mine = oracle.crc32(body[lo:hi])
+        crc = sharded_large_crc(dist, mine, hi - lo)
+        allc = [None] * world
+        dist.all_gather_object(allc, crc)
+        if rank == 0:
+            q.put((allc, oracle.crc32(body)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_large(world, on_gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_large_worker, args=(r, world, port, q, on_gpu)) for r in range(world)]
+    for p in procs:
+        p.start()
+    allc, want = q.get(timeout=110)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert allc == [want] * world
+
+
+def test_gloo_world2_sharded_large_body():
+    """One 24 MiB body cut into two ranges: one all_gather of (crc, len), folded with
+    rpc_crc32_combine on every rank, equals the whole body's CRC."""
+    _run_large(2, on_gpu=False)
+
+
+@pytest.mark.gpu
+def test_gloo_world2_sharded_large_body_hip():
+    """The same through rpc_crc32_device_large per rank (two ranks on cuda:0)."""
+    _run_large(2, on_gpu=True)
