@@ -67,7 +67,9 @@ size_t big_route_workspace_bytes(uint64_t n);
 BigRoute big_route_carve(void *ws, uint64_t n);
 // Before the rows pass: flags and lists the big bodies (route.routed goes into
 // the rows pass's ItemsArgs).  Stream-ordered, no host round trip.
-hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, const BigRoute &r, hipStream_t s);
+// big_min: bodies of at least this many bytes are routed (kBigMin by default).
+hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big_min, const BigRoute &r,
+                               hipStream_t s);
 // After the rows pass: chunk plan, chunk CRCs (rows kernel, RAW), per-body
 // fold into out[batch index].
 hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,

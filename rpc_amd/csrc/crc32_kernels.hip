@@ -544,11 +544,12 @@ hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes,
 // ---------------------------------------------------------------------------
 namespace {
 
-__global__ void __launch_bounds__(256) big_classify_kernel(const uint32_t *lengths, uint64_t n, BigRoute r) {
+__global__ void __launch_bounds__(256) big_classify_kernel(const uint32_t *lengths, uint64_t n, uint32_t big_min,
+                                                             BigRoute r) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t len = (i < n) ? lengths[i] : 0u;
-  const bool big = i < n && len >= kBigMin;
+  const bool big = i < n && len >= big_min;
   const uint64_t m = __builtin_amdgcn_ballot_w64(big);
   uint64_t routed = 0;
   if (m != 0) { // wave-uniform: one slot claim per wave
@@ -697,12 +698,13 @@ BigRoute big_route_carve(void *ws, uint64_t n) {
   return r;
 }
 
-hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, const BigRoute &r, hipStream_t s) {
+hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big_min, const BigRoute &r,
+                               hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (n > kMaxLaunchItems) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(r.meta, 0, 32, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(big_classify_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lengths, n, r);
+  hipLaunchKernelGGL(big_classify_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lengths, n, big_min, r);
   return hipGetLastError();
 }
 

@@ -330,6 +330,13 @@ const uint64_t g_large_chunk = [] {
   return (v >= 16 && v % 16 == 0 && v <= (1ull << 31)) ? (uint64_t)v : (uint64_t)16384;
 }();
 const bool g_large_chunk_env = getenv("RPCCRC_LARGE_CHUNK") != nullptr;
+// Ragged bodies of at least this many bytes take the on-device chunk route
+// (DESIGN.md 4.6).  Tuning override: RPCCRC_BIG_MIN (bytes, >= 16 KiB).
+const uint32_t g_big_min = [] {
+  const char *e = getenv("RPCCRC_BIG_MIN");
+  const unsigned long long v = e ? strtoull(e, nullptr, 10) : 0ull;
+  return (v >= 16384 && v <= 0xFFFFFFFFull) ? (uint32_t)v : kBigMin;
+}();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kPackedMinBodies = 64;         // fewer frames: one wave per body (rows kernel)
 constexpr bool kAutoSplitFrames = true;           // AUTO frames batches: split (true) or packed (false)
@@ -536,9 +543,9 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   BigRoute r{};
   if (route) {
     r = big_route_carve(ws.ptr() + split_bytes, n);
-    RPCCRC_TRY(launch_big_classify(lengths, n, r, s));
+    RPCCRC_TRY(launch_big_classify(lengths, n, g_big_min, r, s));
     a.routed = r.routed;
-    a.big_min = kBigMin;
+    a.big_min = g_big_min;
   }
   if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
