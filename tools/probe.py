@@ -180,7 +180,9 @@ def packed_modes(a):
     dev = torch.device("cuda", 0)
     res = []
     shapes = [("4096x1M", 1 << 20, 4096), ("1024x1M", 1 << 20, 1024), ("3000x1M", 1 << 20, 3000),
-              ("frames1M", 1 << 20, None), ("c2", None, None)]
+              ("frames1M", 1 << 20, None), ("c2", None, None),
+              # multi-row ragged items (whole rows only): 4 / 16 rows per body
+              ("16384x256K", 1 << 18, 16384), ("65536x64K", 1 << 16, 65536)]
     if a.shapes:
         shapes = [x for x in shapes if x[0] in a.shapes.split(",")]
     for name, n, L in shapes:
