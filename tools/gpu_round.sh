@@ -64,6 +64,8 @@ for s in $STEPS; do
     bench_c2_rows) run bench_c2_rows 600 python bench.py --config c2 --ragged-path rows --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
     timeline) run timeline 300 python tools/probe.py --mode timeline --reps 3 ;;
     timeline_c1) run timeline_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 ;;
+    timeline_steal) run timeline_steal_ns 300 python tools/probe.py --mode timeline --reps 3 --steal &&
+                    run timeline_steal_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 --steal ;;
     ablate_mem) run ablate_mem 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl19_d1,qb1_pair1_nt1_abl259_d1,qb1_pair1_nt1_abl275_d1 ;;
     ablate_g) run ablate_g 600 python tools/probe.py --mode ablate --rounds 3 --only qb1_pair1_nt1_abl0_d1,qb1_pair1_nt1_abl0_d1_g1,qb1_pair1_nt1_abl0_d1_g2,qb1_pair1_nt1_abl0_d1_g3,qb1_pair1_nt1_abl0_d1_g4,qb1_pair1_nt1_abl0_d1_g5,qb1_pair1_nt1_abl3_d1,qb1_pair1_nt1_abl3_d1_g5,qb1_pair1_nt1_abl19_d1_g5 ;;
     ablate_g_c1) run ablate_g_c1 600 python tools/probe.py --mode ablate --rounds 3 --config c1 --only qb4_pair1_nt1_abl0_d1,qb4_pair1_nt1_abl0_d1_g1,qb4_pair1_nt1_abl0_d1_g2,qb4_pair1_nt1_abl0_d1_g3,qb4_pair1_nt1_abl0_d1_g4,qb4_pair1_nt1_abl0_d1_g5 ;;

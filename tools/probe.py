@@ -132,7 +132,8 @@ def timeline(w, a):
 
     def f():
         rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1,
-                                  512 | (1024 if a.dyn else 0), 1, 256, s.cuda_stream, times.data_ptr(), a.gshift)
+                                  512 | (1024 if a.dyn or a.steal else 0) | (4096 if a.steal else 0), 1, 256,
+                                  s.cuda_stream, times.data_ptr(), a.gshift)
         assert rc == 0, rc
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
@@ -160,7 +161,7 @@ def timeline(w, a):
         if a.save:
             np.save(f"{a.save}_rep{rep}.npy", np.stack([ent, img, ext]))
         print(json.dumps({"mode": "timeline", "config": a.config, "rep": rep, "qb": qb, "waves": int(live.sum()),
-                          "gshift": a.gshift, "dyn": a.dyn, "exit_median_per_xcd": per_xcd,
+                          "gshift": a.gshift, "dyn": a.dyn, "steal": a.steal, "exit_median_per_xcd": per_xcd,
                           "exit_median_per_wave_slot": per_wave_slot,
                           "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
                           "entry_us_p0_50_99_100": pct(ent), "image_ready_us": pct(img),
@@ -352,6 +353,7 @@ def main():
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
     ap.add_argument("--gshift", type=int, default=0, help="timeline: group-dealing shift of the rows kernel")
     ap.add_argument("--dyn", action="store_true", help="timeline: workgroup-dynamic dealing (DYN)")
+    ap.add_argument("--steal", action="store_true", help="timeline: DYN with the product's tail stealing")
     ap.add_argument("--save", default="", help="timeline: save per-wave times to <save>_rep<k>.npy")
     a = ap.parse_args()
     torch.cuda.set_device(0)

@@ -26,11 +26,27 @@ int ensure_tables() {
   return 0;
 }
 
-// abl bit 1024 (not a kernel ABL bit) selects the workgroup-dynamic dealing (DYN).
+// abl bit 1024 (not a kernel ABL bit) selects the workgroup-dynamic dealing (DYN);
+// 4096 (with 1024) adds the product's tail stealing (15 % of the rounds in the
+// pool, a probe-owned counter that each launch's last workgroup resets).
 constexpr int kProbeDyn = 1024;
+constexpr int kProbeSteal = 4096;
+uint32_t *g_steal = nullptr;
 template <int QB, bool NT, int ABL, int DEPTH>
 void go(const ItemsArgs &a, int blocks, hipStream_t s) {
-  if constexpr ((ABL & kProbeDyn) != 0)
+  if constexpr ((ABL & kProbeSteal) != 0) {
+    if (!g_steal) {
+      if (hipMalloc(&g_steal, 256) != hipSuccess || hipMemset(g_steal, 0, 256) != hipSuccess) return;
+    }
+    ItemsArgs k = a;
+    const uint64_t tasks = QB == 4 ? (a.n_items + 3) / 4 : a.n_items;
+    const uint64_t rounds = (tasks + kDynRound - 1) / kDynRound;
+    const uint64_t st = (uint64_t)((double)rounds * 0.85) / (uint64_t)blocks;
+    k.steal = g_steal;
+    k.steal_s = (uint32_t)st;
+    hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, false, (ABL & ~(kProbeDyn | kProbeSteal)), DEPTH, true, true>),
+                       dim3(blocks), dim3(1024), 0, s, k);
+  } else if constexpr ((ABL & kProbeDyn) != 0)
     hipLaunchKernelGGL((crc32_rows_kernel<QB, NT, false, (ABL & ~kProbeDyn), DEPTH, true>), dim3(blocks), dim3(1024),
                        0, s, a);
   else
@@ -67,6 +83,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_times(const uin
   V(1, 1, 0, 2) V(1, 0, 0, 2) V(1, 1, 3, 2) V(1, 1, 8, 1) V(1, 1, 11, 1) V(1, 1, 9, 1) V(1, 0, 11, 1) V(1, 0, 3, 1) V(1, 1, 16, 1) V(1, 1, 19, 1) V(1, 1, 32, 1) V(1, 1, 35, 1) V(1, 1, 51, 1) V(1, 1, 64, 1) V(1, 1, 128, 1) V(1, 1, 192, 1) V(1, 1, 67, 1) V(1, 1, 131, 1) V(1, 1, 195, 1)
   V(4, 1, 0, 1) V(4, 0, 0, 1) V(4, 1, 3, 1) V(4, 1, 4, 1) V(4, 1, 6, 1) V(4, 1, 0, 2) V(4, 1, 3, 2)
   V(1, 1, 259, 1) V(1, 1, 275, 1) V(1, 1, 512, 1) V(4, 1, 512, 1)
+  V(1, 1, 5632, 1) V(4, 1, 5632, 1)
   V(1, 1, 1024, 1) V(1, 1, 1027, 1) V(1, 1, 1043, 1) V(1, 1, 1536, 1) V(4, 1, 1024, 1) V(4, 1, 1536, 1)
   V(1, 1, 1025, 1) V(1, 1, 1026, 1) V(1, 1, 1028, 1) V(1, 1, 1056, 1) V(1, 1, 1059, 1)
   V(4, 1, 1027, 1) V(4, 1, 1043, 1) V(4, 1, 1028, 1) V(1, 1, 3072, 1) V(4, 1, 3072, 1) V(1, 1, 1040, 1) V(4, 1, 1040, 1)
