@@ -452,7 +452,10 @@ constexpr uint32_t kDynSlots = 4;
 // workgroup consumes its claimed rounds in publication order, so a claim that
 // returns late is never lost.  A wave never waits (for a queue entry or a
 // ring slot) while it holds an unpublished claim.
-constexpr uint32_t kStealAhead = 2;
+#ifndef RPCCRC_STEAL_AHEAD
+#define RPCCRC_STEAL_AHEAD 1
+#endif
+constexpr uint32_t kStealAhead = RPCCRC_STEAL_AHEAD;
 constexpr uint32_t kStealQ = 16;                      // LDS queue ring
 constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
 constexpr uint32_t kStealSpinMax = 1u << 21;          // safety net (~0.1 s): end the wave rather than hang
