@@ -452,6 +452,9 @@ constexpr uint32_t kDynSlots = 4;
 // workgroup consumes its claimed rounds in publication order, so a claim that
 // returns late is never lost.  A wave never waits (for a queue entry or a
 // ring slot) while it holds an unpublished claim.
+#ifndef RPCCRC_STEAL_EXIT_ACQREL
+#define RPCCRC_STEAL_EXIT_ACQREL 0
+#endif
 #ifndef RPCCRC_STEAL_AHEAD
 #define RPCCRC_STEAL_AHEAD 1
 #endif
@@ -621,15 +624,24 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     return n_tasks;
   };
   // Every workgroup passes here once at the end; the last one resets the
-  // device counter for the next launch that leases it.
+  // device counter for the next launch that leases it.  Relaxed: a workgroup
+  // gets here only after every claim it issued has returned (performed), so
+  // the last arrival's reset follows every claim of the launch; the next
+  // launch sees the zeros through the kernel boundary's release.  (acq_rel /
+  // release put an L2 writeback + invalidate, buffer_wbl2 / buffer_inv sc1,
+  // into every workgroup's exit -- RPCCRC_STEAL_EXIT_ACQREL=1 restores it.)
   auto steal_exit = [&]() {
     if (!steal) return;
     __syncthreads();
     if (threadIdx.x == 0) {
+#if RPCCRC_STEAL_EXIT_ACQREL
       const uint32_t old = __hip_atomic_fetch_add(a.steal + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#else
+      const uint32_t old = __hip_atomic_fetch_add(a.steal + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       if (old + 1u == nblk) {
         __hip_atomic_store(a.steal, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.steal + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.steal + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   };
