@@ -452,6 +452,12 @@ constexpr uint32_t kDynSlots = 4;
 // workgroup consumes its claimed rounds in publication order, so a claim that
 // returns late is never lost.  A wave never waits (for a queue entry or a
 // ring slot) while it holds an unpublished claim.
+// Ragged QB = 1: a multi-row item's next row reuses its metadata (no
+// offset / length reload and wait per row).
+#ifndef RPCCRC_META_REUSE
+#define RPCCRC_META_REUSE 1
+#endif
+constexpr bool kRowsMetaReuse = RPCCRC_META_REUSE != 0;
 #ifndef RPCCRC_STEAL_EXIT_ACQREL
 #define RPCCRC_STEAL_EXIT_ACQREL 0
 #endif
@@ -849,9 +855,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
     // more: the wave may still get work (stealing: a task past n inside a
     // pool round is skipped, not the end).  Invalid rows take one step each.
+    // cur_*: the current row's item metadata, reused for the item's next row
+    // (RAGGED: no reload of its offset / length -- a scalar-load wait in
+    // front of every row's loads otherwise).
     auto succ = [&](bool ok, bool more, uint32_t item, uint32_t r, uint32_t nr, uint32_t &s_item, uint32_t &s_r,
                     bool &s_ok, bool &s_more, uint64_t &p0, uint32_t &lp, uint32_t &len, uint32_t &z,
-                    uint32_t &snr, uint32_t &seed) {
+                    uint32_t &snr, uint32_t &seed, uint64_t cur_p0, uint32_t cur_lp, uint32_t cur_len,
+                    uint32_t cur_z, uint32_t cur_seed) {
       const bool adv = r + 1 < nr;
       if constexpr (STEAL) {
         if (adv) {
@@ -889,7 +899,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         s_ok = ok && s_item < n;
         s_more = s_ok;
       }
-      meta(s_ok ? s_item : first_task, p0, lp, len, z, snr, seed);
+      if (kRowsMetaReuse && RAGGED && adv) {
+        p0 = cur_p0;
+        lp = cur_lp;
+        len = cur_len;
+        z = cur_z;
+        snr = nr;
+        seed = cur_seed;
+      } else {
+        meta(s_ok ? s_item : first_task, p0, lp, len, z, snr, seed);
+      }
       if (steal && !s_ok) snr = 1u;
       s_r = adv ? r + 1 : 0u;
     };
@@ -921,7 +940,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
         bool m_ok, m_more;
-        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
+        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, c_p0,
+             c_lp, c_len, c_z, c_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
         fix_row(c_lp, c_z, c_nr, c_r, cb);
         transpose(cb);
@@ -962,7 +982,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
         bool m_ok, m_more;
-        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
+        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, c_p0,
+             c_lp, c_len, c_z, c_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
         compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
         publish();
@@ -990,14 +1011,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       uint32_t n_r, n_len, n_z, n_nr, n_seed;
       bool n_ok, n_more;
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      succ(true, true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed);
+      succ(true, true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed, c_p0, c_lp,
+           c_len, c_z, c_seed);
       issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) {
         uint32_t m_item, m_lp;
         uint64_t m_p0;
         uint32_t m_r, m_len, m_z, m_nr, m_seed;
         bool m_ok, m_more;
-        succ(n_ok, n_more, n_item, n_r, n_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed);
+        succ(n_ok, n_more, n_item, n_r, n_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, n_p0,
+             n_lp, n_len, n_z, n_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
         compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, c_item, cb);
         c_ok = n_ok;
