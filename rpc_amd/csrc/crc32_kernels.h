@@ -43,12 +43,6 @@ struct ItemsArgs {
   // combine XORs into them afterwards).
   uint32_t *zero_out = nullptr;
   uint32_t zero_n = 0;
-  // Uniform RAW batches of 4 KiB chunks dealt in DYN rounds (QB = 1): the wave
-  // completing a round folds its 32 chunk CRCs into ONE crc0 of the round's
-  // 128 KiB and stores it at out[first task / 32] (large bodies: the combine
-  // then folds 2048 partials per 256 MiB instead of 65536).  launch_rows
-  // refuses it for launches that would not deal in DYN rounds.
-  uint32_t fold32 = 0;
 };
 
 // ---- big bodies of a ragged batch ----------------------------

@@ -264,8 +264,6 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   const bool dyn = n_tasks >= 8ull * kDynRound * blocks;
   // Tail stealing (DYN, host-counted): the last steal_frac of the
   // rounds go to the device-counter pool, the rest stay static per workgroup.
-  if (a.fold32 && (!dyn || QB != 1 || a.offsets != nullptr || a.len != 4096 || a.n_items % kDynRound != 0))
-    return hipErrorInvalidValue;
   ItemsArgs k = a;
   k.steal_s = 0;
   if (dyn && a.steal != nullptr && a.n_dev == nullptr) {

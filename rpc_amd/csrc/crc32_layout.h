@@ -17,7 +17,7 @@ namespace rpccrc {
 
 constexpr uint32_t kLdsMain = 0;
 constexpr uint32_t kLdsMainRegion1 = 65536;
-constexpr uint32_t kLdsBytesV2 = 160784;     // rows-kernel image (157 KiB)
+constexpr uint32_t kLdsBytesV2 = 158736;     // rows-kernel image (155 KiB)
 constexpr uint32_t kMaxRow = 4096;           // 64 lanes x 64-byte segments
 constexpr uint32_t kTqEntries = kMaxRow + 1; // Tq[q] = A_q(0xFFFFFFFF), q=0..4096
 
@@ -50,11 +50,7 @@ constexpr uint32_t kLdsZI2 = kLdsRW2 + 512;   // 150016
 constexpr uint32_t kLdsTQ16 = kLdsZI2 + 15 * 512; // 157696
 // A zero dword (TQ16's 12-byte tail pad): lanes with nothing to look up read it.
 constexpr uint32_t kLdsZero = kLdsTQ16 + 1028;
-// FOLD 2 KiB   FOLD[j][n][nib] = A_{8192 * 2^j}(nib << 4n), j = 0..3: with RW
-//              (A_4096) the five Horner levels that fold a round of 32
-//              consecutive 4 KiB chunk CRCs into one (ItemsArgs::fold32).
-constexpr uint32_t kLdsFold = kLdsTQ16 + 1040; // 158736
-static_assert(kLdsFold + 2048 == kLdsBytesV2, "rows image size");
+static_assert(kLdsTQ16 + 1040 == kLdsBytesV2, "rows image size");
 static_assert(kLdsBytesV2 % 16 == 0 && kLdsBytesV2 <= 163840, "fits the 160 KiB LDS");
 void build_lds_image_v2(uint32_t *img /* kLdsBytesV2 bytes */);
 

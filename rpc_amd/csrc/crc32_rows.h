@@ -776,26 +776,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       const uint32_t base = steal ? tsk & ~(kDynRound - 1u) : (rnd * nblk + vb) * kDynRound;
       const uint32_t cnt = (n_tasks - base < kDynRound) ? n_tasks - base : kDynRound;
       if (old + 1u == cnt) { // this wave completed the round
-        uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
-        if (a.fold32) {
-          // lanes 0..31 hold the round's 32 chunk CRCs (crc0, in order): five
-          // Horner levels, level j: lane 2^(j+1) m takes A_{4096 * 2^j} of its
-          // own value XOR its partner's (lane + 2^j); lane 0 ends with crc0 of
-          // the whole round.  One nibble map (8 lookups) per lane per level.
-#pragma unroll
-          for (uint32_t j = 0; j < 5; ++j) {
-            const uint32_t tab = (j == 0) ? kLdsRW2 : kLdsFold + (j - 1u) * 512u;
-            uint32_t m = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) m ^= lds_ld(lds, tab + q * 64u + ((v >> (4u * q)) & 15u) * 4u);
-            v = m ^ (uint32_t)__shfl_down((int)v, 1u << j, 64);
-          }
-          if constexpr ((ABL & kRowsAblNoStore) == 0) {
-            if (lane == 0) store_out(a.out + base / kDynRound, v);
-          } else {
-            sink ^= v;
-          }
-        } else if constexpr ((ABL & kRowsAblNoStore) == 0) {
+        const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
+        if constexpr ((ABL & kRowsAblNoStore) == 0) {
           if (lane < cnt) store_out(a.out + oidx(base + lane), v);
         } else {
           sink ^= v;

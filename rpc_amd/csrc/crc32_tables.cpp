@@ -57,11 +57,6 @@ void build_lds_image_v2(uint32_t *img) {
       for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsZI2 + (z - 1) * 512 + n * 64 + nib * 4, nt[n][nib]);
   }
   for (uint32_t k = 0; k <= 256; ++k) put(kLdsTQ16 + 4 * k, gf2_shift_bytes(0xFFFFFFFFu, 16ull * k));
-  for (uint32_t j = 0; j < 4; ++j) {
-    nibble_table(8192u << j, nt);
-    for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsFold + j * 512 + n * 64 + nib * 4, nt[n][nib]);
-  }
 }
 
 void build_scalar_tab(uint32_t *tab) {

@@ -451,14 +451,6 @@ ItemsArgs items_args(const DeviceCtx &c, const uint8_t *base, const uint64_t *of
 // is a marker packet between back-to-back kernels (+4 us per C1 step with
 // per-step events, profiles/r02/r02aj_step_events_ab.txt).
 // RPCCRC_STEAL_EXT_EVENT=0 records it separately (A/B only).
-// Large bodies: in-kernel round fold (RPCCRC_FOLD32=0 turns it off; A/B only).
-bool fold32_enabled() {
-  static const bool v = [] {
-    const char *e = getenv("RPCCRC_FOLD32");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
 bool steal_ext_event() {
   static const bool v = [] {
     const char *e = getenv("RPCCRC_STEAL_EXT_EVENT");
@@ -690,19 +682,13 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   uint8_t *ws = wsl.ptr();
   uint32_t *d_raw = reinterpret_cast<uint32_t *>(ws);
   uint64_t *d_lens = nullptr, *d_firsts = nullptr;
-  // 4 KiB chunks dealt in DYN rounds of 32: the rows pass folds each round
-  // into one 128 KiB partial (ItemsArgs::fold32), the combine then takes
-  // 2048 partials per 256 MiB body with one block per body.
-  const bool fold = contig && chunk == 4096 && total % 32 == 0 && total <= kMaxLaunchItems &&
-                    total >= 8ull * 32ull * (uint64_t)max_blocks_for(c) && fold32_enabled();
   if (fast) {
     ItemsArgs k = items_args(c, d_base + h_offsets[0], nullptr, nullptr, total, chunk, (uint32_t)chunk, kModeRaw, d_raw);
     StealLease sl; // one-row chunks deal like the north star (items())
     if (chunk <= 4096)
       if (const int rc = sl.get(c, total, 1, s)) return rc;
     k.steal = sl.p;
-    k.fold32 = fold ? 1u : 0u;
-    if (contig && !fold) {
+    if (contig) {
       k.zero_out = d_out;
       k.zero_n = (uint32_t)n;
     }
@@ -736,10 +722,7 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   ca.chunk = chunk;
   ca.out = d_out;
   ca.splits = (uint32_t)splits;
-  if (fold) { // partials of 128 KiB, one combine block per body (plain store)
-    ca.chunk = chunk * 32;
-    for (uint64_t i = 0; i < n; ++i) ib.b[i].chunk_first /= 32;
-  } else if (contig) {
+  if (contig) {
     ca.contig = true;
     ca.splits = (uint32_t)cs;
   }
