@@ -441,7 +441,17 @@ struct QuarterInfo {
 // kDynSlots rounds; the wave completing a round stores its 32 CRCs as one
 // whole 128-B line.
 constexpr uint32_t kDynRound = 32;
-constexpr uint32_t kDynSlots = 4;
+// Rounds the LDS output ring holds: a wave that finishes a task of round r
+// waits until round r - kDynSlots has been stored.  8 (was 4): C2 -1.0 %, NS
+// -0.25 % (profiles/r02/r02bx_dyn_slots_ab.txt); the QB = 4 ring then takes
+// 4 KiB, which still fits beside the 155 KiB image.
+#ifndef RPCCRC_DYN_SLOTS
+#define RPCCRC_DYN_SLOTS 8
+#endif
+#ifndef RPCCRC_DYN_SLOTS_QB1
+#define RPCCRC_DYN_SLOTS_QB1 RPCCRC_DYN_SLOTS
+#endif
+constexpr uint32_t dyn_slots(int QB) { return QB == 1 ? RPCCRC_DYN_SLOTS_QB1 : RPCCRC_DYN_SLOTS; }
 // Tail stealing (DYN with a.steal_s > 0): workgroup vb keeps only its first
 // steal_s local rounds static (global rounds r * blocks + vb); the remaining
 // global rounds form a pool that workgroups claim one round at a time from a
@@ -468,7 +478,7 @@ constexpr uint32_t kStealAhead = RPCCRC_STEAL_AHEAD;
 constexpr uint32_t kStealQ = 16;                      // LDS queue ring
 constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
 constexpr uint32_t kStealSpinMax = 1u << 21;          // safety net (~0.1 s): end the wave rather than hang
-constexpr uint32_t dyn_ring_words(int QB) { return 1 + 2 * kDynSlots + kDynSlots * kDynRound * (uint32_t)QB; }
+constexpr uint32_t dyn_ring_words(int QB) { return 1 + 2 * dyn_slots(QB) + dyn_slots(QB) * kDynRound * (uint32_t)QB; }
 constexpr uint32_t dyn_ctl_words(int QB) { return dyn_ring_words(QB) + kStealCtlWords; }
 
 template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool DYN = false, bool STEAL = false>
@@ -476,6 +486,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   static_assert(!DYN || DEPTH == 1, "DYN: DEPTH = 1");
   static_assert(!STEAL || DYN, "stealing: DYN launches");
+  constexpr uint32_t kDynSlots = dyn_slots(QB);
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
   // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
   // rounds (generation), then the CRC ring (QB CRCs per task).
