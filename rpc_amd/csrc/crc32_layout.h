@@ -37,13 +37,21 @@ constexpr bool kTwoChains = RPCCRC_TWO_CHAINS != 0;
 //               ST1 + (n/2)*4096 + nib*256 + (n%2)*128 + c*4: one v_perm_b32 of
 //               the masked nibble vector forms the address (like MAIN), the
 //               n/2 part rides in the ds_read immediate offset
-//   ST2  2 KiB  ST2[n][nib][hi] = A_{1024*(3-hi)}(nib << 4n),    hi = 0..3
+//   ST2  2 KiB  ST2(n, nib, hi) = A_{1024*(3-hi)}(nib << 4n),    hi = 0..3 (st2_byte)
 //   RW  512 B   RW[n][nib]      = A_4096(nib << 4n)
 //   ZI  7.5 KiB ZI[z-1][n][nib] = A_z^-1(nib << 4n)
 //   TQ16 1 KiB  TQ16[k]         = A_{16k}(0xFFFFFFFF), k = 0..256
 constexpr uint32_t kLdsST1 = 131072;
 constexpr uint32_t kLdsST2 = kLdsST1 + 16384; // 147456
 constexpr uint32_t kLdsRW2 = kLdsST2 + 2048;  // 149504
+// ST2 word of entry (n, nib, k) (k = the shift's quarter index): the 16 nibbles of
+// (n, k) share ONE bank, 2n + (k & 1) + 16 (k >> 1), so the rows kernel's
+// distributed step -- lane (lo = n, hi = k) looks up its own (n, k) -- is
+// bank-conflict-free whatever the nibbles (the [n][nib][k] layout put lanes
+// with equal nibbles on one bank).
+constexpr uint32_t st2_byte(uint32_t n, uint32_t nib, uint32_t k) {
+  return kLdsST2 + 4u * (nib * 32u + 2u * n + (k & 1u) + 16u * (k >> 1));
+}
 constexpr uint32_t kLdsZI2 = kLdsRW2 + 512;   // 150016
 // TQ16[k] = A_{16k}(0xFFFFFFFF), k = 0..256: zlib pre-conditioning seeds for
 // first rows of 16k bytes (other lengths: round up, undo with ZI).

@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   const uint32_t pofs = 16u * piece_of_lane(lane);
   // distributed-step lane constants (the lane looks up nibble lo & 7)
   const uint32_t nshift = 4u * (lo & 7u);
-  const uint32_t n256 = (lo & 7u) * 256u, n64 = (lo & 7u) * 64u;
+  const uint32_t n64 = (lo & 7u) * 64u;
   const bool own = lo < 8u;                // looks up its own row's value
   const bool wlane = hi == 0u && lo >= 8u; // looks up the carried W
   const uint32_t hi8 = 8u * hi;
@@ -374,8 +374,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
       uint32_t a_w;
       if (!cont) a_w = kLdsZero;
       else if (e[0] == 3u) a_w = kLdsRW2 + n64 + nib * 4u;            // A_4096
-      else a_w = kLdsST2 + n256 + (2u - e[0]) * 4u + nib * 16u;       // A_{1024*(e0+1)}
-      const uint32_t a_own = kLdsST2 + n256 + (3u - d) * 4u + nib * 16u; // A_{1024*d}
+      else a_w = st2_byte(lo & 7u, nib, 2u - e[0]);                   // A_{1024*(e0+1)}
+      const uint32_t a_own = st2_byte(lo & 7u, nib, 3u - d);              // A_{1024*d}
       addr = own ? a_own : (wlane ? a_w : kLdsZero);
     }
     const uint32_t t = dist_reduce8(lds_ld(lds, addr));

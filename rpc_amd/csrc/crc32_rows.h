@@ -302,8 +302,8 @@ __device__ __forceinline__ uint32_t dist_reduce8(uint32_t t) {
 struct DistLane {
   uint32_t shift;  // 4 * (lane & 7): which nibble this lane looks up
   uint32_t n64;    // (lane & 7) * 64: nibble-table row ([n][nib] tables, 64 B per n)
-  uint32_t row_base; // merge step: lo < 8 -> ST2 + lo*256 + hi*4; hi == 0, lo >= 8 -> RW2 + (lo-8)*64; else kLdsZero
-  uint32_t row_mul;  // merge step: nibble stride (16 for ST2, 4 for RW2, 0 for the zero lanes)
+  uint32_t row_base; // merge step: lo < 8 -> st2_byte(lo, 0, hi); hi == 0, lo >= 8 -> RW2 + (lo-8)*64; else kLdsZero
+  uint32_t row_mul;  // merge step: nibble stride (128 for ST2, 4 for RW2, 0 for the zero lanes)
   bool own;          // merge step: lane looks up its own row's value (lo < 8)
 };
 
@@ -313,8 +313,8 @@ __device__ __forceinline__ DistLane dist_lane(uint32_t lane) {
   d.shift = 4u * (lane & 7u);
   d.n64 = (lane & 7u) * 64u;
   d.own = lo < 8u;
-  d.row_base = d.own ? kLdsST2 + lo * 256u + hi * 4u : (hi == 0u ? kLdsRW2 + (lo - 8u) * 64u : kLdsZero);
-  d.row_mul = d.own ? 16u : (hi == 0u ? 4u : 0u);
+  d.row_base = d.own ? st2_byte(lo, 0u, hi) : (hi == 0u ? kLdsRW2 + (lo - 8u) * 64u : kLdsZero);
+  d.row_mul = d.own ? st2_byte(0u, 1u, 0u) - st2_byte(0u, 0u, 0u) : (hi == 0u ? 4u : 0u);
   return d;
 }
 

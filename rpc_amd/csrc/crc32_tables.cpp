@@ -46,7 +46,7 @@ void build_lds_image_v2(uint32_t *img) {
   for (uint32_t hi = 0; hi < 4; ++hi) {
     nibble_table(1024u * (3u - hi), nt);
     for (int n = 0; n < 8; ++n)
-      for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsST2 + n * 256 + nib * 16 + hi * 4, nt[n][nib]);
+      for (uint32_t nib = 0; nib < 16; ++nib) put(st2_byte(n, nib, hi), nt[n][nib]);
   }
   nibble_table(4096u, nt);
   for (int n = 0; n < 8; ++n)

@@ -227,8 +227,8 @@ static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
     for (int l = 0; l < 64; ++l) {
       const uint32_t lo = l & 15, hi = l >> 4;
       const bool own = lo < 8;
-      const uint32_t base = own ? kLdsST2 + lo * 256u + hi * 4u : (hi == 0 ? kLdsRW2 + (lo - 8u) * 64u : kLdsZero);
-      const uint32_t mul = own ? 16u : (hi == 0 ? 4u : 0u);
+      const uint32_t base = own ? st2_byte(lo, 0u, hi) : (hi == 0 ? kLdsRW2 + (lo - 8u) * 64u : kLdsZero);
+      const uint32_t mul = own ? st2_byte(0u, 1u, 0u) - st2_byte(0u, 0u, 0u) : (hi == 0 ? 4u : 0u);
       const uint32_t src = own ? s[l] : W;
       t[l] = ld(base + ((src >> (4 * (l & 7))) & 15u) * mul);
     }
@@ -470,8 +470,8 @@ static void emu_packed(const std::vector<const uint8_t *> &ptr, const std::vecto
         const uint32_t nib = ((own ? v : W) >> (4 * n8)) & 15u;
         const uint32_t d = e[hi] - hi;
         const uint32_t a_w = !cont ? kLdsZero
-                             : (e[0] == 3 ? kLdsRW2 + n8 * 64 + nib * 4 : kLdsST2 + n8 * 256 + (2 - e[0]) * 4 + nib * 16);
-        const uint32_t a_own = kLdsST2 + n8 * 256 + (3 - d) * 4 + nib * 16;
+                             : (e[0] == 3 ? kLdsRW2 + n8 * 64 + nib * 4 : st2_byte(n8, nib, 2 - e[0]));
+        const uint32_t a_own = st2_byte(n8, nib, 3 - d);
         t[l] = ld(own ? a_own : (wl ? a_w : kLdsZero));
       }
       dist_reduce8(t);
