@@ -32,7 +32,7 @@
 // LDS image (crc32_layout.h "v3"):
 //   MAIN [0,128K)  slice-by-4 tables x32 copies (two tables per 256-B row)
 //   ST1  16 KiB    A_{64*(15-(c&15))}(nib<<4n), c = lane&31, perm-addressable
-//   ST2  2 KiB     ST2[n][nib][hi] = A_{1024*(3-hi)}(nib<<4n)
+//   ST2  2 KiB     ST2(n, nib, hi) = A_{1024*(3-hi)}(nib<<4n), one bank per (n, hi) (st2_byte)
 //   RW   512 B     RW[n][nib]      = A_4096(nib<<4n)
 //   ZI   7.5 KiB   ZI[z-1][n][nib] = A_z^-1(nib<<4n)
 #pragma once
