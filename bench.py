@@ -67,7 +67,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="ns", choices=sorted(CONFIGS))
+    p.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                   help="default: ns (the north star) at --gpus 1, c3 (BASELINE configs[3]: 8M x 4 KiB per GPU, "
+                        "64M over 8 GPUs) at --gpus > 1")
     p.add_argument("--nontemporal", type=int, default=-1, help="-1 = library default")
     p.add_argument("--ragged-path", default="auto", choices=["auto", "rows", "packed", "split"],
                    help="ragged-batch kernel (C2): auto = rows for device batches; packed = 1 KiB chunks four per row")
@@ -90,7 +92,14 @@ def parse():
     p.add_argument("--prewarm-s", type=float, default=0.5,
                    help="untimed steps before the W warmup steps until this much time has passed: the GPU "
                         "clock ramps over the first ~20 launches of sustained load (DESIGN.md 5)")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.config is None:
+        # BASELINE.json: the north star is quoted at 1 GPU; configs[3] (64M x 4 KiB
+        # sharded evenly over 8 GPUs) is the multi-GPU workload -- 8M bodies per
+        # rank at every N > 1 (weak scaling).
+        world = int(os.environ.get("WORLD_SIZE", "0")) or args.gpus
+        args.config = "c3" if max(world, args.gpus) > 1 else "ns"
+    return args
 
 
 class Workload:
@@ -174,9 +183,24 @@ def cgroup_cpu_quota():
         return None
 
 
+def effective_cpus():
+    """(CPUs of throughput this process really has, CPUs in its affinity mask): the
+    affinity mask capped by the cgroup's cpu.max quota (a 256-thread host that grants
+    16 CPUs' worth of time is a 16-CPU baseline, VERDICT r02 #7)."""
+    aff = max(1, len(os.sched_getaffinity(0)))
+    q = cgroup_cpu_quota()
+    return (max(1, min(aff, int(math.ceil(q)))) if q else aff), aff
+
+
+# Samples larger than the host's last-level cache (AMD EPYC 9575F: 8 x 32 MiB L3),
+# so the baseline streams from DRAM as the GPU streams from HBM.
+CPU_SAMPLE_BYTES = 1 << 30
+
+
 def cpu_baseline(w: Workload, target_s: float):
     """The reference crc.c (+ system libz, built into oracle/_ref) timed on this
-    host's cores over a bounded sample of the same workload."""
+    host's cores over a bounded sample of the same workload, at 1 thread and at
+    the effective CPU count (affinity mask capped by the cgroup quota)."""
     from oracle import oracle  # cpu_baseline leg only (test/baseline infrastructure)
     import zlib
 
@@ -184,16 +208,16 @@ def cpu_baseline(w: Workload, target_s: float):
     kind = "reference"
     if ref is None:
         return None
-    threads = max(1, len(os.sched_getaffinity(0)))  # every CPU this process may run on
+    threads, aff = effective_cpus()
     if w.kind == "uniform":
-        nb = min(w.n, (256 << 20) // w.L)
+        nb = min(w.n, CPU_SAMPLE_BYTES // w.L)
         host = w.base[: nb * w.L].cpu().numpy()
         offs = np.arange(nb, dtype=np.uint64) * np.uint64(w.L)
         lens = np.full(nb, w.L, dtype=np.uint32)
         sample = f"{nb} x {w.L} B bodies (first {nb * w.L >> 20} MiB of the same device stream)"
         dev_crc = w.out[:nb].cpu().numpy().view(np.uint32)
     elif w.kind == "ragged":
-        nb = int(np.searchsorted(np.cumsum(w.lens_h, dtype=np.uint64), 256 << 20))
+        nb = int(np.searchsorted(np.cumsum(w.lens_h, dtype=np.uint64), CPU_SAMPLE_BYTES))
         end = int(w.offs_h[nb - 1] + w.lens_h[nb - 1])
         host = w.base[:end].cpu().numpy()
         offs, lens = w.offs_h[:nb], w.lens_h[:nb]
@@ -215,24 +239,41 @@ def cpu_baseline(w: Workload, target_s: float):
     if sm > 0:
         reps = max(1, min(5000, int(math.ceil(target_s / sm))))
     sm, _ = ref.batch_timed(host, offs, lens, threads=threads, reps=reps)
+    # Labelled extra only: the same sample on every CPU of the affinity mask
+    # (quota bursting; not the baseline).
+    all_aff = None
+    if aff > threads:
+        ta, _ = ref.batch_timed(host, offs, lens, threads=aff, reps=max(1, reps // 4))
+        all_aff = {"threads": aff, "GiBps": round(nbytes * max(1, reps // 4) / ta / GiB, 3)}
     # Config C0, the reference's own CPU case: 1024 x 4 KiB
-    # JSON-RPC bodies, crc.c at 1 thread and at `threads`, ~1 s each; the GPU's
-    # CRCs of the same bodies are checked equal.
+    # JSON-RPC bodies, crc.c at 1 thread and at the effective CPU count; the
+    # GPU's CRCs of the same bodies are checked equal.  Timed over the 4 MiB set
+    # tiled to 1 GiB, so the sample exceeds the L3 (a 4 MiB set is cache-resident
+    # and let 256 threads burst past the quota).
     c0_buf, c0_offs, c0_lens = oracle.json_bodies(1024, 4096, 0x5EED0001)
     c0_bytes = int(c0_lens.sum(dtype=np.uint64))
-    c0 = {"sample": "1024 x 4096 B JSON-RPC bodies (seed 0x5EED0001)"}
+    _, c0_crc = ref.batch_timed(c0_buf, c0_offs, c0_lens, threads=1, reps=1)
+    tiles = max(1, CPU_SAMPLE_BYTES // c0_bytes)
+    c0_big = np.tile(c0_buf, tiles)
+    c0_boffs = np.arange(1024 * tiles, dtype=np.uint64) * np.uint64(4096)
+    c0_blens = np.full(1024 * tiles, 4096, dtype=np.uint32)
+    c0 = {"sample": f"1024 x 4096 B JSON-RPC bodies (seed 0x5EED0001), the set tiled {tiles}x "
+                    f"({c0_bytes * tiles >> 20} MiB) so it exceeds the L3"}
     for tn in sorted({1, threads}):
-        t1, c0_crc = ref.batch_timed(c0_buf, c0_offs, c0_lens, threads=tn, reps=1)
-        r = max(1, min(20000, int(math.ceil(1.0 / max(t1, 1e-6)))))
-        tr, _ = ref.batch_timed(c0_buf, c0_offs, c0_lens, threads=tn, reps=r)
-        c0[f"GiBps_{tn}_threads"] = round(c0_bytes * r / tr / GiB, 3)
+        t1, _ = ref.batch_timed(c0_big, c0_boffs, c0_blens, threads=tn, reps=1)
+        r = max(1, min(200, int(math.ceil(1.0 / max(t1, 1e-6)))))
+        tr, _ = ref.batch_timed(c0_big, c0_boffs, c0_blens, threads=tn, reps=r)
+        c0[f"GiBps_{tn}_threads"] = round(c0_bytes * tiles * r / tr / GiB, 3)
+    del c0_big
     c0_dev = rpc_amd.device_uniform(torch.from_numpy(c0_buf).to(w.device), 1024, 4096)
     c0["gpu_crcs_match_reference"] = bool(np.array_equal(c0_dev.cpu().numpy().view(np.uint32), c0_crc))
     return {
         "value": round(nbytes * reps / sm / GiB, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "cores_source": f"min(affinity mask {aff}, ceil(cgroup cpu.max quota {cgroup_cpu_quota()}))",
         "cgroup_cpu_quota": cgroup_cpu_quota(),
+        "all_affinity_threads": all_aff,
         "kind": kind,
         "c0": c0,
         "sample": f"{sample}, {reps} passes on {threads} threads ({sm:.1f} s)",
@@ -473,7 +514,7 @@ def main():
         sys.exit(self_launch(args))
     if os.environ.get("RPCCRC_BENCH_LAUNCH_ONLY"):  # CPU rehearsal of the launch path (tests/test_bench_launch.py)
         print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus,
-                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+                          "master": os.environ.get("MASTER_ADDR"), "config": args.config}), flush=True)
         return
     _load_gpu_modules()
     from rpc_amd.shard import barrier, max_over_ranks, sum_over_ranks

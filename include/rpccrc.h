@@ -47,7 +47,8 @@ extern "C" {
 #define RPCCRC_EINVAL (-22) /* bad argument (NULL buffer with n>0, bad size, ...) */
 #define RPCCRC_ENODEV (-19) /* no usable HIP device */
 #define RPCCRC_ENOMEM (-12) /* device or pinned allocation failed */
-#define RPCCRC_EIO (-5)     /* HIP runtime / kernel launch error */
+#define RPCCRC_EIO (-5)     /* HIP runtime / kernel launch error, or a kernel-reported
+                               device error (rpc_crc32_device_status) */
 #define RPCCRC_EAGAIN (-11) /* receive ring: no free segment yet, poll first */
 
 /* ---- drop-in (reference crc.h) ---------------------------------------- */
@@ -117,6 +118,16 @@ RPCCRC_API int rpc_crc32_device_large(const uint8_t *d_base, const uint64_t *h_o
                                   peer is dropped before its body is read
                                   (rpc_server_main.c:189-195, rpc_async.c:312) */
 #define RPC_FRAME_MALFORMED 4u /* header or body extends past the stream: not read */
+#define RPC_FRAME_RECV_ERR 5u  /* client role only: a non-PONG frame with body_len 0.
+                                  The reference client's BODY state then calls
+                                  recv(fd, buf, 0), which returns 0; it takes that for
+                                  the peer closing (rpc_async.c:330-349), drops the
+                                  connection and completes the call with RPC_RECV_ERR
+                                  (rpc_types.h:26, rpc_async.c:377-386).
+                                  rpc_crc32_verify (rpc_async.c:219) is never reached.
+                                  The server reads an empty body and verifies it
+                                  (rpc_server_main.c:198-227), so a server-role frame
+                                  with body_len 0 is OK / BAD_CRC by its crc32 field. */
 
 /* Frame-call flags.  The role picks which heartbeat type is a control frame
  * (the other one is an ordinary data frame, as in the reference). */
@@ -181,10 +192,10 @@ RPCCRC_API void rpc_rx_ring_destroy(rpc_rx_ring_t *ring);
  * still in flight or unpolled (call rpc_rx_ring_poll). */
 RPCCRC_API int rpc_rx_ring_reserve(rpc_rx_ring_t *ring, size_t frame_len, uint8_t **dst);
 /* Accepts the reserved frame; RPCCRC_EINVAL (frame dropped) unless the landed
- * length is what the reference reads for that header: 12 + body_len for a data
- * frame, or the 12-byte header alone for a control frame or a data frame over
+ * length is exactly what the reference reads for that header: 12 + body_len for
+ * a data frame, the 12-byte header alone for a control frame or a data frame over
  * the cap (the reference reads no body for either, rpc_server_main.c:172-195,
- * rpc_async.c:303-315). */
+ * rpc_async.c:303-315; the bytes after such a header belong to the next frame). */
 RPCCRC_API int rpc_rx_ring_commit(rpc_rx_ring_t *ring, uint64_t tag);
 /* reserve + memcpy + commit. */
 RPCCRC_API int rpc_rx_ring_push(rpc_rx_ring_t *ring, const void *frame, size_t frame_len, uint64_t tag);
@@ -233,6 +244,14 @@ RPCCRC_API const char *rpc_crc32_strerror(int err);
 
 /* Writes "device=<name> arch=<gcn> cus=<n>" for the current device. */
 RPCCRC_API int rpc_crc32_device_info(char *buf, size_t buflen);
+
+/* Sticky device status of the current device: RPCCRC_OK, or RPCCRC_EIO once a
+ * kernel has stored into the library's device error word (a bounded wait of the
+ * rows kernel's dealing protocol ran out, so CRCs of that launch may be stale).
+ * Like a sticky HIP error it stays set for the life of the process, and every
+ * later call on the device returns RPCCRC_EIO (the drop-in calls abort).  Device
+ * calls are asynchronous: check after synchronising the stream. */
+RPCCRC_API int rpc_crc32_device_status(void);
 
 #ifdef __cplusplus
 }

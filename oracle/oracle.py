@@ -96,7 +96,7 @@ def crc32_uniform(buf: np.ndarray, n: int, body_len: int, stride: int | None = N
 
 # ---- frame verdicts (the reference's receive-side decisions) -------------------
 
-FRAME_BAD_CRC, FRAME_OK, FRAME_CONTROL, FRAME_TOO_LARGE, FRAME_MALFORMED = 0, 1, 2, 3, 4
+FRAME_BAD_CRC, FRAME_OK, FRAME_CONTROL, FRAME_TOO_LARGE, FRAME_MALFORMED, FRAME_RECV_ERR = 0, 1, 2, 3, 4, 5
 MAX_BODY_LEN = 1024  # rpc.h:17
 RPC_TYPE_PING, RPC_TYPE_PONG = 1, 2  # rpc.h:12-13
 
@@ -107,8 +107,12 @@ def frame_verdict(stream: bytes, off: int, role: str = "server", lift_cap: bool 
     a server answers PING from the header alone (rpc_server_main.c:172-187), a client
     consumes PONG the same way (rpc_async.c:303-309); a body_len over MAX_BODY_LEN drops
     the peer before the body is read (rpc_server_main.c:189-195, rpc_async.c:312-315);
-    otherwise the body is read and rpc_crc32_verify decides (rpc_server_main.c:227,
-    rpc_async.c:219).  MALFORMED: the frame does not fit the stream (our bound)."""
+    a client that gets body_len 0 enters its BODY state, whose recv(fd, buf, 0) returns
+    0 -- taken for a closed peer (rpc_async.c:330-349), so the call ends with
+    RPC_RECV_ERR (rpc_types.h:26) and no verify: RECV_ERR (the server reads the empty
+    body and verifies it, rpc_server_main.c:198-227); otherwise the body is read and
+    rpc_crc32_verify decides (rpc_server_main.c:227, rpc_async.c:219).  MALFORMED: the
+    frame does not fit the stream (our bound)."""
     if off + 12 > len(stream):
         return FRAME_MALFORMED, 0
     h = stream[off:off + 12]
@@ -119,6 +123,8 @@ def frame_verdict(stream: bytes, off: int, role: str = "server", lift_cap: bool 
         return FRAME_CONTROL, 0
     if blen > MAX_BODY_LEN and not lift_cap:
         return FRAME_TOO_LARGE, 0
+    if blen == 0 and role == "client":
+        return FRAME_RECV_ERR, 0
     if off + 12 + blen > len(stream):
         return FRAME_MALFORMED, 0
     c = crc32(np.frombuffer(stream, dtype=np.uint8)[off + 12:off + 12 + blen]) if blen else 0

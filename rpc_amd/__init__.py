@@ -41,6 +41,7 @@ __all__ = [
     "set_options",
     "set_ragged_path",
     "device_info",
+    "device_status",
     "RPC_HEADER_LEN",
     "RPC_TYPE_DATA",
     "RPC_TYPE_PING",
@@ -51,6 +52,7 @@ __all__ = [
     "FRAME_CONTROL",
     "FRAME_TOO_LARGE",
     "FRAME_MALFORMED",
+    "FRAME_RECV_ERR",
 ]
 
 # reference rpc.h:11-17
@@ -66,6 +68,7 @@ FRAME_OK = 1
 FRAME_CONTROL = 2
 FRAME_TOO_LARGE = 3
 FRAME_MALFORMED = 4
+FRAME_RECV_ERR = 5  # client role, body_len 0: rpc_async.c:330-349 drops the connection (RPC_RECV_ERR)
 FRAMES_SERVER = 0x1
 FRAMES_CLIENT = 0x2
 FRAMES_LIFT_CAP = 0x4
@@ -272,6 +275,11 @@ def set_ragged_path(path="auto"):
     one wavefront per body)."""
     code = RAGGED_PATHS[path] if isinstance(path, str) else int(path)
     check(_lib.rpc_crc32_set_ragged_path(code), "rpc_crc32_set_ragged_path")
+
+
+def device_status() -> int:
+    """0, or -5 (RPCCRC_EIO) once a kernel has reported a device error (sticky)."""
+    return int(_lib.rpc_crc32_device_status())
 
 
 def device_info() -> str:

@@ -69,6 +69,7 @@ rpc_crc32_set_options = _sig("rpc_crc32_set_options", _i32, _i32, _i32)
 rpc_crc32_set_ragged_path = _sig("rpc_crc32_set_ragged_path", _i32, _i32)
 rpc_crc32_strerror = _sig("rpc_crc32_strerror", ctypes.c_char_p, _i32)
 rpc_crc32_device_info = _sig("rpc_crc32_device_info", _i32, ctypes.c_char_p, _sz)
+rpc_crc32_device_status = _sig("rpc_crc32_device_status", _i32)
 
 #: Every symbol include/rpccrc.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -95,6 +96,7 @@ EXPORTS = (
     "rpc_crc32_set_ragged_path",
     "rpc_crc32_strerror",
     "rpc_crc32_device_info",
+    "rpc_crc32_device_status",
 )
 
 

@@ -43,7 +43,19 @@ struct ItemsArgs {
   // combine XORs into them afterwards).
   uint32_t *zero_out = nullptr;
   uint32_t zero_n = 0;
+  // Device error word of the launch's device (pinned host memory, zero while
+  // all is well).  A wave whose bounded wait in the DYN / tail-stealing
+  // protocol runs out stores kErr* into it (crc32_rows.h); the host turns a
+  // non-zero word into RPCCRC_EIO (sticky per device, rpc_crc32_device_status).
+  uint32_t *err = nullptr;
+  // Test-only (RPCCRC_TEST_STEAL_GIVEUP=1 in the environment): every pool-round
+  // wait gives up at once, so the error path can be exercised deliberately.
+  uint32_t test_giveup = 0;
 };
+
+// Device error bits (ItemsArgs.err).
+constexpr uint32_t kErrStealWait = 1u; // a wave gave up waiting for a stolen round: its tasks were not run
+constexpr uint32_t kErrRingWait = 2u;  // a wave gave up waiting for an output-ring slot: CRCs may be stale
 
 // ---- big bodies of a ragged batch ----------------------------
 // One wave per body would leave a long body streaming through a single wave

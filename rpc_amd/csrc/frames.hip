@@ -33,7 +33,10 @@ __device__ __forceinline__ bool inside(uint64_t off, uint64_t len, uint64_t byte
 // rpc_async.c:312), then the body is read and its CRC checked
 // (rpc_server_main.c:227, rpc_async.c:219).  A frame whose body is not read gets
 // length 0 here (its CRC is then 0) and its final verdict now; data frames get
-// kFramePending and are decided by frames_compare_kernel.
+// kFramePending and are decided by frames_compare_kernel.  The client drops a
+// data frame with body_len 0 before verifying it: its BODY state recv()s 0
+// bytes, gets 0 back and takes that for a closed peer (rpc_async.c:330-349 ->
+// RPC_RECV_ERR), so that case is RPC_FRAME_RECV_ERR.
 __global__ void frames_parse_kernel(const uint8_t *stream, uint64_t stream_bytes, const uint64_t *frame_off,
                                     uint64_t n, int flags, uint64_t *body_off, uint32_t *body_len, uint32_t *hdr_crc,
                                     uint8_t *pre) {
@@ -54,6 +57,8 @@ __global__ void frames_parse_kernel(const uint8_t *stream, uint64_t stream_bytes
       v = RPC_FRAME_CONTROL;
     else if (bl > RPC_MAX_BODY_LEN && !(flags & RPC_FRAMES_LIFT_CAP))
       v = RPC_FRAME_TOO_LARGE;
+    else if (bl == 0 && (flags & RPC_FRAMES_CLIENT))
+      v = RPC_FRAME_RECV_ERR;
     else if (!inside(off + kFrameHeaderLen, bl, stream_bytes))
       v = RPC_FRAME_MALFORMED;
     else

@@ -180,43 +180,42 @@ struct Lease {
 // vs r02af_bench_c1.log).
 class StealPool {
  public:
-  int acquire(hipStream_t s, uint32_t **p, int *slot, hipEvent_t *ev) {
-    int k = -1;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      if (free_.size() < kMinFree)
-        if (const int rc = grow()) return rc;
-      k = free_.front();
-      free_.pop_front();
-    }
-    Slot &x = all_[k];
-    if (x.used && hipEventQuery(x.ev) != hipSuccess) RPCCRC_TRY(hipStreamWaitEvent(s, x.ev, 0));
-    *p = x.p;
-    *slot = k;
-    *ev = x.ev;
-    return RPCCRC_OK;
-  }
-  // recorded: the launch recorded the slot's event as its completion signal
-  // (launch_rows steal_done).  Otherwise the slot may have been used by a
-  // launch without it (ext_event() off): record it here, a marker packet.
-  void release(int k, hipStream_t s, bool recorded, bool dealt) {
-    Slot &x = all_[k];
-    if (recorded) {
-      x.used = true;
-    } else if (dealt) {
-      x.used = hipEventRecord(x.ev, s) == hipSuccess;
-      if (!x.used) (void)hipStreamSynchronize(s);
-    } // else the launch did not touch the slot: its last use (and event) stand
-    std::lock_guard<std::mutex> g(mu_);
-    free_.push_back(k);
-  }
-
- private:
   struct Slot {
     uint32_t *p = nullptr;
     hipEvent_t ev = nullptr;
     bool used = false;
   };
+  // The lessee gets the Slot itself (taken under mu_), so no lookup of the
+  // slot storage happens outside the lock while grow() may be extending it
+  // (deque operator[] outside mu_ raced with push_back).
+  int acquire(hipStream_t s, Slot **out) {
+    Slot *x = nullptr;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (free_.size() < kMinFree)
+        if (const int rc = grow()) return rc;
+      x = free_.front();
+      free_.pop_front();
+    }
+    if (x->used && hipEventQuery(x->ev) != hipSuccess) RPCCRC_TRY(hipStreamWaitEvent(s, x->ev, 0));
+    *out = x;
+    return RPCCRC_OK;
+  }
+  // recorded: the launch recorded the slot's event as its completion signal
+  // (launch_rows steal_done).  Otherwise the slot may have been used by a
+  // launch without it (ext_event() off): record it here, a marker packet.
+  void release(Slot *x, hipStream_t s, bool recorded, bool dealt) {
+    if (recorded) {
+      x->used = true;
+    } else if (dealt) {
+      x->used = hipEventRecord(x->ev, s) == hipSuccess;
+      if (!x->used) (void)hipStreamSynchronize(s);
+    } // else the launch did not touch the slot: its last use (and event) stand
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(x);
+  }
+
+ private:
   static constexpr int kChunk = 64;
   static constexpr size_t kMinFree = 16; // grow early: a slot rests >= 16 leases before reuse
   int grow() { // under mu_
@@ -227,14 +226,14 @@ class StealPool {
       Slot x;
       x.p = reinterpret_cast<uint32_t *>(mem + 256 * i);
       RPCCRC_TRY(hipEventCreateWithFlags(&x.ev, hipEventDisableTiming));
-      free_.push_back((int)all_.size());
       all_.push_back(x);
+      free_.push_back(&all_.back());
     }
     return RPCCRC_OK;
   }
   std::mutex mu_;
-  std::deque<Slot> all_; // references stay valid as it grows (slots are used outside mu_)
-  std::deque<int> free_;  // FIFO: least recently used first
+  std::deque<Slot> all_;   // element addresses stay valid as it grows; touched only under mu_
+  std::deque<Slot *> free_; // FIFO: least recently used first
 };
 
 // A simple free list of T (one borrower at a time, created on demand).
@@ -269,8 +268,6 @@ struct ScalarCtx {
   uint32_t *pout = nullptr; // pinned result (rows kernel path)
   uint64_t *pres = nullptr; // pinned {crc, seq} of the one-wave kernel (polled)
   uint32_t seq = 0;
-  uint8_t *dbuf = nullptr;  // device staging for large bodies
-  size_t dcap = 0;
 };
 
 // rpc_crc32_batch: two slots, each a stream with a device stage and pinned
@@ -301,6 +298,11 @@ struct DeviceCtx {
   uint32_t *tq = nullptr;
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
   uint4 *scalar_tab = nullptr; // one-wave scalar kernel's table image (kScalarTabWords)
+  // Device error word (pinned, coherent host memory): the rows kernel stores
+  // kErr* here when a bounded wait runs out (crc32_rows.h).  Sticky: once it is
+  // non-zero every call on this device returns RPCCRC_EIO (the drop-in calls
+  // abort), like a sticky HIP error -- CRCs of the failed launch may be stale.
+  uint32_t *err = nullptr;
   int status = RPCCRC_ENODEV;
   char name[128] = {0};
   char arch[64] = {0};
@@ -386,6 +388,8 @@ void init_device(int dev) {
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.scalar_tab, kScalarTabWords * 4) : e;
+  e = (e == hipSuccess) ? hipHostMalloc(reinterpret_cast<void **>(&c.err), 64, hipHostMallocCoherent) : e;
+  if (e == hipSuccess) *reinterpret_cast<volatile uint32_t *>(c.err) = 0;
   if (e == hipSuccess) {
     build_lds_image_v2(img.data());
     e = hipMemcpy(c.img, img.data(), kLdsBytesV2, hipMemcpyHostToDevice);
@@ -402,6 +406,11 @@ void init_device(int dev) {
   c.status = map_hip(e);
 }
 
+// Sticky device error (DeviceCtx::err): RPCCRC_EIO once a kernel has reported one.
+int device_error(const DeviceCtx &c) {
+  return (c.err != nullptr && *reinterpret_cast<const volatile uint32_t *>(c.err) != 0u) ? RPCCRC_EIO : RPCCRC_OK;
+}
+
 // Context of the calling thread's current device.
 int get_ctx(DeviceCtx **out) {
   int dev = -1;
@@ -410,7 +419,18 @@ int get_ctx(DeviceCtx **out) {
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RPCCRC_ENODEV;
   std::call_once(g_once[dev], init_device, dev);
   *out = &g_dev[dev];
-  return g_dev[dev].status;
+  if (g_dev[dev].status != RPCCRC_OK) return g_dev[dev].status;
+  return device_error(g_dev[dev]);
+}
+
+// Test-only: RPCCRC_TEST_STEAL_GIVEUP=1 makes every tail-stealing pool-round
+// wait give up (ItemsArgs.test_giveup), to exercise the device error word.
+uint32_t test_giveup() {
+  static const uint32_t v = [] {
+    const char *e = getenv("RPCCRC_TEST_STEAL_GIVEUP");
+    return (e && e[0] == '1') ? 1u : 0u;
+  }();
+  return v;
 }
 
 int max_blocks_for(const DeviceCtx &c) {
@@ -437,6 +457,8 @@ ItemsArgs items_args(const DeviceCtx &c, const uint8_t *base, const uint64_t *of
   a.tq = c.tq;
   a.out = out;
   a.gshift = kRowsGroupShift;
+  a.err = c.err;
+  a.test_giveup = test_giveup();
   return a;
 }
 
@@ -460,11 +482,10 @@ bool steal_ext_event() {
 }
 struct StealLease {
   StealPool *pool = nullptr;
-  int slot = -1;
+  StealPool::Slot *slot = nullptr;
   hipStream_t s = nullptr;
   uint32_t *p = nullptr;
-  hipEvent_t ev = nullptr;
-  bool recorded = false; // the launch recorded ev itself
+  bool recorded = false; // the launch recorded the slot's event itself
   StealLease() = default;
   StealLease(const StealLease &) = delete;
   StealLease &operator=(const StealLease &) = delete;
@@ -474,12 +495,13 @@ struct StealLease {
   int get(const DeviceCtx &c, uint64_t n, int QB, hipStream_t stream) {
     const uint64_t tasks = QB == 4 ? (n + 3) / 4 : n;
     if (tasks < 8ull * 32ull * (uint64_t)max_blocks_for(c)) return RPCCRC_OK;
-    if (const int rc = c.steal->acquire(stream, &p, &slot, &ev)) return rc;
+    if (const int rc = c.steal->acquire(stream, &slot)) return rc;
+    p = slot->p;
     pool = c.steal;
     s = stream;
     return RPCCRC_OK;
   }
-  hipEvent_t done_event() const { return steal_ext_event() ? ev : nullptr; }
+  hipEvent_t done_event() const { return steal_ext_event() && slot ? slot->ev : nullptr; }
 };
 
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
@@ -815,30 +837,32 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
   if (len <= kScalarZeroCopyMax) {
     memcpy(t->pin, src, len);
     rc = items(*c, t->pin, nullptr, nullptr, 1, 0, len, kModeFinal, t->pout, 1, t->stream);
+    if (rc) die("kernel launch", rc);
   } else {
-    if (t->dcap < len) {
-      if (t->dbuf) (void)hipFree(t->dbuf);
-      t->dbuf = nullptr;
-      t->dcap = 0;
-      if (hipMalloc(reinterpret_cast<void **>(&t->dbuf), len) != hipSuccess) die("device alloc", RPCCRC_ENOMEM);
-      t->dcap = len;
-    }
-    if (hipMemcpyAsync(t->dbuf, src, len, hipMemcpyHostToDevice, t->stream) != hipSuccess) die("H2D copy", RPCCRC_EIO);
+    // Device staging borrowed from the device's workspace pool (stream-ordered
+    // reuse: no hipMalloc / hipFree -- a hipFree synchronises the whole device
+    // and stalls every other thread's stream).  The CRC lands
+    // in a device word at the end of the lease and comes back by a 4-byte D2H
+    // copy: the chunk combine XORs its partials in with device atomics, which
+    // must not target host memory.
+    const size_t body = (len + 255) & ~(size_t)255;
+    Lease stage;
+    if ((rc = stage.get(c->ws, body + 256, t->stream))) die("device staging", rc);
+    uint8_t *dbuf = stage.ptr();
+    uint32_t *dword = reinterpret_cast<uint32_t *>(dbuf + body);
+    if (hipMemcpyAsync(dbuf, src, len, hipMemcpyHostToDevice, t->stream) != hipSuccess) die("H2D copy", RPCCRC_EIO);
     if (len >= kScalarChunkedMin) {
       const uint64_t off = 0, l64 = len;
-      rc = device_large(*c, t->dbuf, &off, &l64, 1, t->pout, 0, t->stream);
+      rc = device_large(*c, dbuf, &off, &l64, 1, dword, 0, t->stream);
     } else {
-      rc = items(*c, t->dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, t->pout, 1, t->stream);
+      rc = items(*c, dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, dword, 1, t->stream);
     }
-  }
-  if (rc) die("kernel launch", rc);
+    if (rc) die("kernel launch", rc);
+    if (hipMemcpyAsync(t->pout, dword, 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess) die("D2H copy", RPCCRC_EIO);
+  } // the lease returns the staging block here, after its last use was enqueued
   if (hipStreamSynchronize(t->stream) != hipSuccess) die("stream sync", RPCCRC_EIO);
+  if ((rc = device_error(*c))) die("kernel (device error word)", rc);
   const uint32_t r = *t->pout;
-  if (t->dcap > (64u << 20)) { // do not keep a huge one-off staging buffer
-    (void)hipFree(t->dbuf);
-    t->dbuf = nullptr;
-    t->dcap = 0;
-  }
   c->scalar->release(t);
   return r;
 }
@@ -935,7 +959,8 @@ int host_batch_run(const DeviceCtx &c, HostPipeline &p, const uint8_t *base, con
 int host_batch(DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
                uint32_t *out) {
   HostPipeline *p = c.pipes->acquire();
-  const int rc = host_batch_run(c, *p, base, offsets, lengths, n, out);
+  int rc = host_batch_run(c, *p, base, offsets, lengths, n, out);
+  if (rc == RPCCRC_OK) rc = device_error(c); // every launch of this call has completed
   if (rc) // leave the pipeline idle for its next borrower
     for (HostSlot &s : p->slot)
       if (s.busy) {
@@ -1114,6 +1139,11 @@ int rpc_crc32_set_ragged_path(int path) {
     return RPCCRC_EINVAL;
   g_ragged_path.store(path);
   return RPCCRC_OK;
+}
+
+int rpc_crc32_device_status(void) {
+  DeviceCtx *c = nullptr;
+  return get_ctx(&c);
 }
 
 const char *rpc_crc32_strerror(int err) {

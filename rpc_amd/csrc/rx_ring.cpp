@@ -207,17 +207,20 @@ int rpc_rx_ring_commit(rpc_rx_ring_t *r, uint64_t tag) {
   const size_t len = r->reserved_len;
   r->reserved = nullptr;
   r->reserved_len = 0;
-  // The landed length must be what the reference reads for this header: the
-  // header alone for a control frame (rpc_server_main.c:172-187 PING at the
-  // server, rpc_async.c:303-309 PONG at the client) or a data frame over the
-  // cap (rpc_server_main.c:189-195, rpc_async.c:312: dropped before the body),
-  // else the header plus body_len bytes (rpc.h:6).
+  // The landed length must be exactly what the reference reads for this
+  // header: the header alone for a control frame (rpc_server_main.c:172-187
+  // PING at the server, rpc_async.c:303-309 PONG at the client) or a data
+  // frame over the cap (rpc_server_main.c:189-195, rpc_async.c:312: dropped
+  // before the body) -- any bytes after such a header are the NEXT frame's to
+  // the reference, so a landing that includes them is refused -- else the
+  // header plus body_len bytes (rpc.h:6).
   const uint64_t bl = be32(h + 4);
   const uint16_t type = be16(h + 2);
   const bool control = (type == RPC_FRAME_TYPE_PING && (r->flags & RPC_FRAMES_SERVER)) ||
                        (type == RPC_FRAME_TYPE_PONG && (r->flags & RPC_FRAMES_CLIENT));
   const bool over_cap = bl > RPC_MAX_BODY_LEN && !(r->flags & RPC_FRAMES_LIFT_CAP);
-  if (len != bl + kHdr && !(len == kHdr && (control || over_cap))) return RPCCRC_EINVAL;
+  const uint64_t want = (control || over_cap) ? kHdr : bl + kHdr;
+  if (len != want) return RPCCRC_EINVAL;
   s.h_off[s.nframes] = s.used;
   s.tags.push_back(tag);
   s.used += len;

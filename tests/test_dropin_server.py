@@ -186,9 +186,15 @@ def test_reference_client_10_threads(server):
     assert rc == 0 and res == {"success": 50, "failure": 0}, err[-2000:]
 
 
-def _bad_crc_server(port_holder, stop):
-    """A server that answers every DATA request with a response whose crc32 field is
-    wrong (and PING with PONG, as the reference server would)."""
+def _bad_crc_reply(req):
+    body = json.dumps({"jsonrpc": "2.0", "id": req["id"], "result": 3}, separators=(",", ":")).encode()
+    return struct.pack(">HHII", 1, 0, len(body), oracle.crc32(body) ^ 0x00010000) + body
+
+
+def _bad_crc_server(port_holder, stop, reply=_bad_crc_reply):
+    """A server that answers every DATA request with reply(request) -- by default a
+    response whose crc32 field is wrong -- and PING with PONG, as the reference
+    server would."""
     ls = socket.socket()
     ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     ls.bind(("127.0.0.1", 0))
@@ -207,8 +213,7 @@ def _bad_crc_server(port_holder, stop):
                     c.sendall(struct.pack(">HHII", ver, 2, 0, 0))
                     continue
                 req = json.loads(recv_exact(c, blen))
-                body = json.dumps({"jsonrpc": "2.0", "id": req["id"], "result": 3}, separators=(",", ":")).encode()
-                c.sendall(struct.pack(">HHII", ver, 0, len(body), oracle.crc32(body) ^ 0x00010000) + body)
+                c.sendall(reply(req))
         except OSError:
             return
         finally:
@@ -237,3 +242,70 @@ def test_reference_client_flags_corrupted_response():
         stop.set()
         t.join(timeout=5)
     assert res == {"status": 5}, err[-2000:]
+
+
+def _run_client_against(reply):
+    """One `client_rpccrc raw` call against a server answering with reply(request);
+    returns the reference client's rpc_error_code."""
+    port, stop = [], threading.Event()
+    t = threading.Thread(target=_bad_crc_server, args=(port, stop, reply), daemon=True)
+    t.start()
+    while not port:
+        time.sleep(0.05)
+    try:
+        rc, res, err = _client("raw", port[0], '{"jsonrpc":"2.0","method":"add_i32","params":{"a":1,"b":2},"id":1}',
+                               timeout=60)
+    finally:
+        stop.set()
+        t.join(timeout=5)
+    return res["status"], err
+
+
+def test_client_verdicts_match_reference_client():
+    """the client-role verdicts pinned against the reference CLIENT itself,
+    as test_batched_verdicts_match_reference_server pins the server role.  A scripted
+    server answers the request with each response below; the reference client library
+    (on librpccrc) completes the call with RPC_OK (0), RPC_RECV_ERR (4) or RPC_CRC_ERR
+    (5) (rpc_types.h:22-27), and rpc_frames_verify_device(role=client) must give the
+    matching verdict for the same bytes:
+      * body_len 0, any non-PONG type: the BODY state's recv of 0 bytes returns 0, read
+        as a closed peer (rpc_async.c:330-349) -> RPC_RECV_ERR <-> FRAME_RECV_ERR;
+      * body_len over MAX_BODY_LEN -> dropped before the body (rpc_async.c:312) -> 4;
+      * a PING carrying a valid body is an ordinary data frame at the client -> OK;
+      * a PONG (junk crc / body_len fields, no body) is consumed from the header alone
+        (rpc_async.c:303-309), then the real response decides."""
+    torch = pytest.importorskip("torch")
+    import rpc_amd
+
+    def good_body(req):
+        return json.dumps({"jsonrpc": "2.0", "id": req["id"], "result": 3}, separators=(",", ":")).encode()
+
+    hdr = lambda t, bl, c: struct.pack(">HHII", 1, t, bl, c)  # noqa: E731
+    cases = [  # (name, reply(req) -> list of frames, expected status)
+        ("empty data", lambda r: [hdr(0, 0, 0)], 4),
+        ("empty data, crc field set", lambda r: [hdr(0, 0, 0x1234ABCD)], 4),
+        ("empty ping", lambda r: [hdr(1, 0, 0)], 4),
+        ("empty unknown type", lambda r: [hdr(7, 0, 0)], 4),
+        ("over cap", lambda r: [hdr(0, 2000, 0)], 4),
+        ("ping with valid body", lambda r: [hdr(1, len(good_body(r)), oracle.crc32(good_body(r))) + good_body(r)], 0),
+        ("bad crc", lambda r: [hdr(0, len(good_body(r)), oracle.crc32(good_body(r)) ^ 4) + good_body(r)], 5),
+        ("pong then response", lambda r: [hdr(2, 777, 0xDEADBEEF),
+                                          hdr(0, len(good_body(r)), oracle.crc32(good_body(r))) + good_body(r)], 0),
+        ("good", lambda r: [hdr(0, len(good_body(r)), oracle.crc32(good_body(r))) + good_body(r)], 0),
+    ]
+    status_of = {rpc_amd.FRAME_OK: 0, rpc_amd.FRAME_RECV_ERR: 4, rpc_amd.FRAME_TOO_LARGE: 4, rpc_amd.FRAME_BAD_CRC: 5}
+    req = {"id": 1}
+    for name, reply, want in cases:
+        status, err = _run_client_against(lambda r, reply=reply: b"".join(reply(r)))
+        assert status == want, (name, status, err[-1500:])
+        frames = reply(req)
+        offs, blob = [], b""
+        for f in frames:
+            offs.append(len(blob))
+            blob += f
+        v, _ = rpc_amd.frames_verify(torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).cuda(),
+                                     torch.tensor(offs, dtype=torch.int64).cuda(), role="client")
+        v = v.cpu().tolist()
+        assert all(x == rpc_amd.FRAME_CONTROL for x in v[:-1]), (name, v)  # heartbeats consumed first
+        assert status_of[v[-1]] == status, (name, v, status)
+        assert v == [oracle.frame_verdict(blob, o, "client")[0] for o in offs], name

@@ -88,19 +88,40 @@ def test_captured_ping_pong(golden):
     v, _ = verify(stream, offs, role="server")
     assert v == [rpc_amd.FRAME_CONTROL, rpc_amd.FRAME_OK]  # a server reads PONG as an (empty) data frame
     v, _ = verify(stream, offs, role="client")
-    assert v == [rpc_amd.FRAME_OK, rpc_amd.FRAME_CONTROL]
+    # a client reads PING as a data frame with body_len 0: recv(fd, buf, 0) == 0 drops
+    # the connection before any verify (rpc_async.c:330-349 -> RPC_RECV_ERR)
+    assert v == [rpc_amd.FRAME_RECV_ERR, rpc_amd.FRAME_CONTROL]
+
+
+@pytest.mark.parametrize("lift_cap", [False, True])
+def test_frames_zero_length_bodies(lift_cap):
+    """body_len 0 of every type and crc32 field: the server verifies the empty body
+    (crc 0 == field? rpc_server_main.c:198-227); the client drops the connection
+    unless the frame is a PONG (rpc_async.c:303-309 vs :330-349)."""
+    frames = [header(0, c, t) for t in (0, 1, 2, 3, 0xFFFF) for c in (0, 1, 0x80000000, 0xFFFFFFFF)]
+    stream, offs = layout(frames, gap=2)
+    for role in ("server", "client"):
+        got = verify(stream, offs, role, lift_cap)
+        assert got == expected(stream, offs, role, lift_cap), role
+    v, _ = verify(stream, offs, "client", lift_cap)
+    assert v == [rpc_amd.FRAME_CONTROL if t == 2 else rpc_amd.FRAME_RECV_ERR
+                 for t in (0, 1, 2, 3, 0xFFFF) for _ in range(4)]
+    v, _ = verify(stream, offs, "server", lift_cap)
+    assert v == [rpc_amd.FRAME_CONTROL if t == 1 else (rpc_amd.FRAME_OK if c == 0 else rpc_amd.FRAME_BAD_CRC)
+                 for t in (0, 1, 2, 3, 0xFFFF) for c in (0, 1, 0x80000000, 0xFFFFFFFF)]
 
 
 @pytest.mark.parametrize("role", ["server", "client"])
 @pytest.mark.parametrize("lift_cap", [False, True])
 def test_frames_type_rules(role, lift_cap):
     """Heartbeats whose crc32 / body_len fields are not zero, unknown types, over-cap
-    lengths: every verdict and CRC equals the reference's decision."""
+    lengths, empty bodies (one frame in eight): every verdict and CRC equals the
+    reference's decision."""
     rng = np.random.default_rng(7 + lift_cap)
     frames = []
     for i in range(600):
         kind = int(rng.integers(0, 8))
-        blen = int(rng.integers(0, 1500))
+        blen = int(rng.integers(0, 1500)) if rng.integers(0, 8) else 0
         body = rng.integers(0, 256, blen, dtype=np.uint8).tobytes()
         crc = oracle.crc32(body)
         if kind == 0:  # PING with junk crc / body_len, landed as the header alone (server reads no body)

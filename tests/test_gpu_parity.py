@@ -62,9 +62,82 @@ def test_drop_in_golden_random(golden):
 
 
 def test_drop_in_large_bodies():
-    for n in [(8 << 20) - 1, (8 << 20) + 13, (17 << 20) + 5]:  # device copy and chunked paths
+    # device copy and chunked paths; exact multiples of 16 MiB take the one-row-chunk
+    # contiguous combine, whose atomics now target a device word, not
+    # the pinned host result
+    for n in [(8 << 20) - 1, (8 << 20) + 13, (17 << 20) + 5, 16 << 20, 32 << 20, 48 << 20]:
         data = oracle.splitmix_bytes(n, n)
         assert rpc_amd.rpc_crc32(data) == oracle.crc32(data), n
+
+
+def test_drop_in_staging_pool_with_concurrent_batch():
+    """the drop-in path stages bodies > 64 KiB in the device workspace
+    pool (stream-ordered, no hipMalloc / hipFree device sync).  > 64 MiB drop-in calls
+    on one thread while another thread runs device batches on its own stream; every
+    CRC checked, twice (the second round reuses the pooled blocks)."""
+    big = [(64 << 20) + 17, (96 << 20), (65 << 20) + 3]
+    datas = [oracle.splitmix_bytes(n, 0xB16 + n) for n in big]
+    wants = [oracle.crc32(d) for d in datas]
+    n, L = 4096, 3000
+    host = oracle.splitmix_bytes(n * L, 0xBA7C4)
+    base = to_dev(host)
+    want_b = oracle.crc32_uniform(host, n, L)
+    errors = []
+    stop = threading.Event()
+
+    def batches():
+        s = torch.cuda.Stream()
+        k = 0
+        while not stop.is_set() or k < 4:
+            with torch.cuda.stream(s):
+                got = u32(rpc_amd.device_uniform(base, n, L, stream=s))
+            if not np.array_equal(got, want_b):
+                errors.append(("batch", k))
+            k += 1
+
+    th = threading.Thread(target=batches)
+    th.start()
+    try:
+        for _ in range(2):
+            for d, w in zip(datas, wants):
+                if rpc_amd.rpc_crc32(d) != w:
+                    errors.append(("drop-in", len(d)))
+    finally:
+        stop.set()
+        th.join()
+    assert not errors, errors
+    assert rpc_amd.device_status() == 0
+
+
+def test_device_error_word_reports_steal_giveup():
+    """a wave that gives up a bounded wait of the tail-stealing
+    protocol stores into the device error word, and the host reports RPCCRC_EIO
+    (sticky) instead of returning stale CRCs with rc 0.  Forced in a child process
+    with the test-only RPCCRC_TEST_STEAL_GIVEUP=1 (every pool round gives up)."""
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import numpy as np, torch, rpc_amd
+torch.cuda.set_device(0)
+n, L = 65536, 4096
+base = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+rpc_amd.fill_random(base, 0x6E7)
+assert rpc_amd.device_status() == 0
+rpc_amd.device_uniform(base, n, L)     # deals its last rounds from the steal pool
+torch.cuda.synchronize()
+print("status", rpc_amd.device_status())
+try:
+    rpc_amd.device_uniform(base, 16, L)
+    print("next", 0)
+except rpc_amd.RpcCrcError as e:
+    print("next", e.code)
+"""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RPCCRC_TEST_STEAL_GIVEUP="1", PYTHONPATH=repo)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=repo)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "status -5" in p.stdout and "next -5" in p.stdout, p.stdout
 
 
 def test_drop_in_frames(golden):

@@ -161,11 +161,15 @@ def test_ring_control_and_over_cap_frames(role):
         (_hdr(500, 0xDEADBEEF, ctl), rpc_amd.FRAME_CONTROL, 1),
         (_hdr(0, 0, ctl), rpc_amd.FRAME_CONTROL, 1),
         (_hdr(2000, 0x1234), rpc_amd.FRAME_TOO_LARGE, 0),
-        (_hdr(1025, 0) + bytes(1025), rpc_amd.FRAME_TOO_LARGE, 0),  # landed whole: still over the cap
+        (_hdr(1025, 0), rpc_amd.FRAME_TOO_LARGE, 0),
         (frame(body), rpc_amd.FRAME_OK, 1),
         (frame(body, type_=other), rpc_amd.FRAME_OK, 1),          # the other heartbeat type is data here
         (frame(body, type_=other, crc=5), rpc_amd.FRAME_BAD_CRC, 0),
-        (frame(b"", type_=other), rpc_amd.FRAME_OK, 1),
+        # an empty body: the server verifies it (crc 0), the client drops the
+        # connection on its recv of 0 bytes (rpc_async.c:330-349, RPC_RECV_ERR)
+        (frame(b"", type_=other), rpc_amd.FRAME_OK if role == "server" else rpc_amd.FRAME_RECV_ERR,
+         1 if role == "server" else 0),
+        (frame(b""), rpc_amd.FRAME_OK if role == "server" else rpc_amd.FRAME_RECV_ERR, 1 if role == "server" else 0),
     ]
     with rpc_amd.RxRing(1 << 16, 64, 2, role=role) as ring:
         for i, (f, _, _) in enumerate(frames):
@@ -173,6 +177,11 @@ def test_ring_control_and_over_cap_frames(role):
         # a data frame landed as a bare header while its body_len is within the cap is refused
         with pytest.raises(rpc_amd.RpcCrcError):
             ring.push(_hdr(100, 0), 99)
+        # a control / over-cap header landed together with bytes after it is refused:
+        # the reference reads the header alone and takes those bytes for the next frame
+        for bad in (_hdr(4, 0, ctl) + b"abcd", _hdr(1025, 0) + bytes(1025)):
+            with pytest.raises(rpc_amd.RpcCrcError):
+                ring.push(bad, 98)
         ring.submit()
         got = ring.poll(wait=True)
     assert [g[0] for g in got] == list(range(len(frames)))
