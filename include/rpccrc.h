@@ -81,6 +81,15 @@ RPCCRC_API int64_t rpc_crc32_verify_batch(const uint8_t *base, const uint64_t *o
 RPCCRC_API int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
                            uint64_t n, uint32_t *d_out, void *stream);
 
+/* rpc_crc32_device_batch with a length bound the caller knows (e.g. MAX_BODY_LEN,
+ * rpc.h:17, or a workload's maximum): max_len >= every d_lengths[i], 0 = none.
+ * With a bound below 256 KiB the big-body chunk route is never needed and its
+ * passes are not launched.  Results never depend on the hint: a body longer
+ * than a wrong bound is still CRC'd exactly (by one wavefront, so slowly). */
+RPCCRC_API int rpc_crc32_device_batch_bounded(const uint8_t *d_base, const uint64_t *d_offsets,
+                                              const uint32_t *d_lengths, uint64_t n, uint32_t max_len,
+                                              uint32_t *d_out, void *stream);
+
 /* Equal-length batch: body i = d_base[i*stride .. + body_len). */
 RPCCRC_API int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_len, uint64_t stride,
                              uint32_t *d_out, void *stream);
@@ -119,12 +128,16 @@ RPCCRC_API int rpc_crc32_device_large(const uint8_t *d_base, const uint64_t *h_o
                                   (rpc_server_main.c:189-195, rpc_async.c:312) */
 #define RPC_FRAME_MALFORMED 4u /* header or body extends past the stream: not read */
 #define RPC_FRAME_RECV_ERR 5u  /* client role only: a non-PONG frame with body_len 0.
-                                  The reference client's BODY state then calls
-                                  recv(fd, buf, 0), which returns 0; it takes that for
-                                  the peer closing (rpc_async.c:330-349), drops the
-                                  connection and completes the call with RPC_RECV_ERR
-                                  (rpc_types.h:26, rpc_async.c:377-386).
-                                  rpc_crc32_verify (rpc_async.c:219) is never reached.
+                                  The reference client's BODY state calls
+                                  recv(fd, buf, 0) on its non-blocking socket; once
+                                  any further byte (or the peer's FIN) is pending that
+                                  returns 0, taken for a closed peer
+                                  (rpc_async.c:330-349): the connection is dropped and
+                                  the call ends with RPC_RECV_ERR (rpc_types.h:26,
+                                  rpc_async.c:377-386).  (On an idle socket recv
+                                  returns EAGAIN and the client waits until more
+                                  arrives, or the call times out.)  The empty body is
+                                  never verified (rpc_async.c:219 is not reached).
                                   The server reads an empty body and verifies it
                                   (rpc_server_main.c:198-227), so a server-role frame
                                   with body_len 0 is OK / BAD_CRC by its crc32 field. */

@@ -107,10 +107,11 @@ def frame_verdict(stream: bytes, off: int, role: str = "server", lift_cap: bool 
     a server answers PING from the header alone (rpc_server_main.c:172-187), a client
     consumes PONG the same way (rpc_async.c:303-309); a body_len over MAX_BODY_LEN drops
     the peer before the body is read (rpc_server_main.c:189-195, rpc_async.c:312-315);
-    a client that gets body_len 0 enters its BODY state, whose recv(fd, buf, 0) returns
-    0 -- taken for a closed peer (rpc_async.c:330-349), so the call ends with
-    RPC_RECV_ERR (rpc_types.h:26) and no verify: RECV_ERR (the server reads the empty
-    body and verifies it, rpc_server_main.c:198-227); otherwise the body is read and
+    a client that gets body_len 0 enters its BODY state, whose recv(fd, buf, 0) on the
+    non-blocking socket returns 0 once anything more (or a FIN) is pending -- taken for
+    a closed peer (rpc_async.c:330-349), so the call ends with RPC_RECV_ERR
+    (rpc_types.h:26) and the empty body is never verified: RECV_ERR (the server reads
+    the empty body and verifies it, rpc_server_main.c:198-227); otherwise the body is read and
     rpc_crc32_verify decides (rpc_server_main.c:227, rpc_async.c:219).  MALFORMED: the
     frame does not fit the stream (our bound)."""
     if off + 12 > len(stream):

@@ -168,14 +168,17 @@ def _dev_u32_out(n: int, device, out):
     return out
 
 
-def device_batch(base, offsets, lengths, out=None, stream=None):
-    """Ragged batch over a device byte tensor; offsets int64/uint64, lengths int32/uint32 device tensors."""
+def device_batch(base, offsets, lengths, out=None, stream=None, max_len: int = 0):
+    """Ragged batch over a device byte tensor; offsets int64/uint64, lengths int32/uint32 device tensors.
+    ``max_len``: an upper bound on the lengths the caller knows (0 = none); below 256 KiB the
+    big-body route's passes are skipped (rpc_crc32_device_batch_bounded; results never depend on it)."""
     n = offsets.numel()
     if lengths.numel() != n:
         raise ValueError("offsets and lengths differ in length")
     out = _dev_u32_out(n, base.device, out)
-    check(_lib.rpc_crc32_device_batch(base.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), n,
-                                      out.data_ptr(), _stream_handle(stream)), "rpc_crc32_device_batch")
+    check(_lib.rpc_crc32_device_batch_bounded(base.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), n,
+                                              int(max_len) & 0xFFFFFFFF, out.data_ptr(), _stream_handle(stream)),
+          "rpc_crc32_device_batch_bounded")
     return out
 
 

@@ -50,6 +50,7 @@ rpc_crc32_verify = _sig("rpc_crc32_verify", ctypes.c_bool, _vp, _sz, _u32)
 rpc_crc32_batch = _sig("rpc_crc32_batch", _i32, _u8p, _vp, _vp, _sz, _vp, _i32)
 rpc_crc32_verify_batch = _sig("rpc_crc32_verify_batch", ctypes.c_int64, _u8p, _vp, _vp, _vp, _sz, _vp)
 rpc_crc32_device_batch = _sig("rpc_crc32_device_batch", _i32, _vp, _vp, _vp, _u64, _vp, _vp)
+rpc_crc32_device_batch_bounded = _sig("rpc_crc32_device_batch_bounded", _i32, _vp, _vp, _vp, _u64, _u32, _vp, _vp)
 rpc_crc32_device_uniform = _sig("rpc_crc32_device_uniform", _i32, _vp, _u64, _u32, _u64, _vp, _vp)
 rpc_crc32_device_large = _sig("rpc_crc32_device_large", _i32, _vp, _vp, _vp, _u64, _vp, _u64, _vp)
 rpc_frames_verify_device = _sig("rpc_frames_verify_device", _i32, _vp, _u64, _vp, _u64, _i32, _vp, _vp, _vp)
@@ -78,6 +79,7 @@ EXPORTS = (
     "rpc_crc32_batch",
     "rpc_crc32_verify_batch",
     "rpc_crc32_device_batch",
+    "rpc_crc32_device_batch_bounded",
     "rpc_crc32_device_uniform",
     "rpc_crc32_device_large",
     "rpc_frames_verify_device",

@@ -343,6 +343,9 @@ constexpr int kRowsAblNoImage = 256;    // no LDS image copy (timing only; with 
 // with the wave's task count; times = a.offsets (unused by uniform batches).
 constexpr int kRowsAblTimes = 512;
 constexpr int kRowsAblNtStore = 2048; // non-temporal CRC stores (DYN paths; exact)
+// Chain only slots 2-3 (8 slice-by-4 steps per lane, the last 2 KiB of the row):
+// the instruction cost of a half-width row (timing only: wrong CRCs).
+constexpr int kRowsAblHalfChain = 8192;
 // QB = 1 software pipeline over rows (chain of row r+1 beside the merge of row r).
 #ifndef RPCCRC_ROWS_PIPE
 #define RPCCRC_ROWS_PIPE 1
@@ -720,6 +723,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // crc0 of quarter hi of the row.
   auto quarter_crcs = [&](u32x4 (&buf)[4]) -> uint32_t {
     if constexpr ((ABL & kRowsAblNoTranspose) == 0) transpose(buf);
+    if constexpr ((ABL & kRowsAblHalfChain) != 0) {
+      uint32_t x = buf[2][0];
+#pragma unroll
+      for (int k = 2; k < 4; ++k)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (k == 2 && d == 0) continue;
+          x = slice4w(lds, x, buf[k][d], lsel);
+        }
+      return merge_lo(lds, slice4(lds, x, lsel), lsel1);
+    }
     if constexpr ((ABL & (kRowsAblNoCompute | kRowsAblNoMerge)) == 0) return row_quarters(lds, buf, lsel, lsel1, upper);
     uint32_t s;
     if constexpr ((ABL & kRowsAblNoCompute) != 0) s = xor_fold(buf);

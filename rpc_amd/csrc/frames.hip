@@ -33,10 +33,10 @@ __device__ __forceinline__ bool inside(uint64_t off, uint64_t len, uint64_t byte
 // rpc_async.c:312), then the body is read and its CRC checked
 // (rpc_server_main.c:227, rpc_async.c:219).  A frame whose body is not read gets
 // length 0 here (its CRC is then 0) and its final verdict now; data frames get
-// kFramePending and are decided by frames_compare_kernel.  The client drops a
-// data frame with body_len 0 before verifying it: its BODY state recv()s 0
-// bytes, gets 0 back and takes that for a closed peer (rpc_async.c:330-349 ->
-// RPC_RECV_ERR), so that case is RPC_FRAME_RECV_ERR.
+// kFramePending and are decided by frames_compare_kernel.  The client never
+// verifies a data frame with body_len 0: its BODY state recv()s 0 bytes, which
+// returns 0 as soon as anything more (or a FIN) is pending on the socket, taken
+// for a closed peer (rpc_async.c:330-349 -> RPC_RECV_ERR): RPC_FRAME_RECV_ERR.
 __global__ void frames_parse_kernel(const uint8_t *stream, uint64_t stream_bytes, const uint64_t *frame_off,
                                     uint64_t n, int flags, uint64_t *body_off, uint32_t *body_len, uint32_t *hdr_crc,
                                     uint8_t *pre) {

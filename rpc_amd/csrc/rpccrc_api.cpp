@@ -1028,12 +1028,23 @@ int64_t rpc_crc32_verify_batch(const uint8_t *base, const uint64_t *offsets, con
 
 int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                            uint32_t *d_out, void *stream) {
+  return rpc_crc32_device_batch_bounded(d_base, d_offsets, d_lengths, n, 0, d_out, stream);
+}
+
+int rpc_crc32_device_batch_bounded(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                                   uint64_t n, uint32_t max_len, uint32_t *d_out, void *stream) {
   if (n == 0) return RPCCRC_OK;
   if (!d_base || !d_offsets || !d_lengths || !d_out) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) return rc;
-  return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream), false, true);
+  // A bound below the route threshold: no body can take the big-body route, so
+  // its passes (classify before the rows pass; plan, expand, chunk rows and
+  // fold after it: ~30 us of launches, profiles/r02final4/c2_kernel_stats.csv)
+  // are not launched.  A body over a wrong bound is still CRC'd correctly by
+  // the rows pass (one wave for the whole body): the hint is about speed only.
+  const bool route = max_len == 0 || max_len >= g_big_min;
+  return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream), false, route);
 }
 
 int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_len, uint64_t stride, uint32_t *d_out,

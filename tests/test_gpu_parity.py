@@ -606,7 +606,22 @@ def test_device_batch_big_bodies_route(path, misalign):
     finally:
         rpc_amd.set_ragged_path("auto")
     host = base.cpu().numpy()
-    assert got.tolist() == oracle.crc32_batch(host, offs_p, lens_p).tolist()
+    want = oracle.crc32_batch(host, offs_p, lens_p).tolist()
+    assert got.tolist() == want
+    # rpc_crc32_device_batch_bounded: a bound under the route threshold skips the
+    # route; a WRONG bound (bodies above it) still gives every exact CRC (one wave
+    # per big body), and the unbounded C entry point agrees
+    d_o, d_l = to_dev(offs_p.view(np.int64)), to_dev(lens_p.view(np.int32))
+    rpc_amd.set_ragged_path(path)
+    try:
+        wrong = u32(rpc_amd.device_batch(base, d_o, d_l, max_len=70000))
+        right = u32(rpc_amd.device_batch(base, d_o, d_l, max_len=max(lens)))
+        plain = torch.empty(len(lens), dtype=torch.int32, device=DEV)
+        assert rpc_amd._lib.rpc_crc32_device_batch(base.data_ptr(), d_o.data_ptr(), d_l.data_ptr(), len(lens),
+                                                   plain.data_ptr(), rpc_amd._stream_handle(None)) == 0
+    finally:
+        rpc_amd.set_ragged_path("auto")
+    assert wrong.tolist() == want and right.tolist() == want and u32(plain).tolist() == want
 
 
 def test_device_batch_route_overflow_and_overlap():

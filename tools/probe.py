@@ -89,6 +89,7 @@ def ablate_variants(w, a):
     # DYN: merge only / chain only / compute only / no transpose / memory only without transpose
     combos += [(1, 1, 1, 1025, 1), (1, 1, 1, 1026, 1), (1, 1, 1, 1028, 1), (1, 1, 1, 1056, 1), (1, 1, 1, 1059, 1)]
     combos += [(1, 1, 1, 3072, 1), (1, 1, 1, 1040, 1)]  # DYN with NT stores / no stores
+    combos += [(1, 1, 1, 9216, 1)]  # DYN, chain of slots 2-3 only: a half-width row's instruction cost
     if w.L <= 1024:  # aligned uniform bodies: z = 0
         combos += [(4, 1, 1, 0, 1), (4, 1, 0, 0, 1), (4, 1, 1, 3, 1), (4, 1, 1, 4, 1), (4, 1, 1, 6, 1),
                    (4, 1, 1, 0, 2), (4, 1, 1, 3, 2)] + [(4, 1, 1, 0, 1, g) for g in (1, 2, 3, 4, 5)] + [(4, 1, 1, 1024, 1), (4, 1, 1, 1027, 1), (4, 1, 1, 1043, 1), (4, 1, 1, 1028, 1), (4, 1, 1, 3072, 1), (4, 1, 1, 1040, 1)]

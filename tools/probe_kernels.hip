@@ -86,7 +86,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_times(const uin
   V(1, 1, 5632, 1) V(4, 1, 5632, 1)
   V(1, 1, 1024, 1) V(1, 1, 1027, 1) V(1, 1, 1043, 1) V(1, 1, 1536, 1) V(4, 1, 1024, 1) V(4, 1, 1536, 1)
   V(1, 1, 1025, 1) V(1, 1, 1026, 1) V(1, 1, 1028, 1) V(1, 1, 1056, 1) V(1, 1, 1059, 1)
-  V(4, 1, 1027, 1) V(4, 1, 1043, 1) V(4, 1, 1028, 1) V(1, 1, 3072, 1) V(4, 1, 3072, 1) V(1, 1, 1040, 1) V(4, 1, 1040, 1)
+  V(1, 1, 9216, 1) V(4, 1, 1027, 1) V(4, 1, 1043, 1) V(4, 1, 1028, 1) V(1, 1, 3072, 1) V(4, 1, 3072, 1) V(1, 1, 1040, 1) V(4, 1, 1040, 1)
   return -22;
 }
 
