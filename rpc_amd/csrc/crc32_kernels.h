@@ -127,6 +127,18 @@ struct CombineArgs {
   InlineBodies bodies;
 };
 
+// Tasks per dealing round of the rows kernel's workgroup-dynamic dealing
+// (crc32_rows.h DYN).
+constexpr uint32_t kDynRound = 32;
+// QB = 4 rounds may be shorter: a round of 16 four-body tasks is still 64
+// whole CRCs (two 128-B lines), and the tail -- the last claimed round per
+// workgroup -- is one task per wave instead of two.
+#ifndef RPCCRC_DYN_ROUND_QB4
+#define RPCCRC_DYN_ROUND_QB4 32
+#endif
+constexpr uint32_t dyn_round(int QB) { return QB == 4 ? (uint32_t)RPCCRC_DYN_ROUND_QB4 : kDynRound; }
+static_assert(RPCCRC_DYN_ROUND_QB4 == 16 || RPCCRC_DYN_ROUND_QB4 == 32, "QB = 4 round: 16 or 32 tasks");
+
 // Most items one rows-kernel launch takes (it indexes them in 32 bits);
 // launch_rows splits larger host-counted batches.
 constexpr uint64_t kMaxLaunchItems = 1ull << 30;

@@ -261,13 +261,14 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // several rounds of 32 tasks; small batches (e.g. the chunks of a few large
   // bodies) keep the static one-task-per-wave dealing.
   const uint64_t n_tasks = (QB == 4) ? (a.n_items + 3) / 4 : a.n_items;
-  const bool dyn = n_tasks >= 8ull * kDynRound * blocks;
+  const uint64_t round = dyn_round(QB);
+  const bool dyn = n_tasks >= 8ull * round * blocks;
   // Tail stealing (DYN, host-counted): the last steal_frac of the
   // rounds go to the device-counter pool, the rest stay static per workgroup.
   ItemsArgs k = a;
   k.steal_s = 0;
   if (dyn && a.steal != nullptr && a.n_dev == nullptr) {
-    const uint64_t rounds = (n_tasks + kDynRound - 1) / kDynRound;
+    const uint64_t rounds = (n_tasks + round - 1) / round;
     const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac())) / blocks;
     if (st >= kStealAhead && st * blocks < rounds) k.steal_s = (uint32_t)st;
   }

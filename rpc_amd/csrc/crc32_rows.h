@@ -252,17 +252,27 @@ __device__ __forceinline__ uint32_t swap_lanebit4(uint32_t v, bool upper) {
 // stays in a register (a conditionally written local array went to scratch:
 // 176 B per lane, the image loaded twice).
 template <uint32_t kBytes>
-__device__ __forceinline__ void copy_lds_image(const uint4 *src, uint4 *dst) {
-  constexpr uint32_t kN16 = kBytes / 16, kFull = kN16 / 1024, kRem = kN16 % 1024;
-  const uint32_t tid = threadIdx.x;
+struct ImageRegs {
+  static constexpr uint32_t kN16 = kBytes / 16, kFull = kN16 / 1024, kRem = kN16 % 1024;
   uint4 t[kFull];
+  uint4 r;
+};
+template <uint32_t kBytes>
+__device__ __forceinline__ void load_lds_image(const uint4 *src, ImageRegs<kBytes> &im) {
+  using I = ImageRegs<kBytes>;
+  const uint32_t tid = threadIdx.x;
 #pragma unroll
-  for (uint32_t i = 0; i < kFull; ++i) t[i] = src[tid + i * 1024u];
-  uint4 r = make_uint4(0, 0, 0, 0);
-  if (kRem != 0 && tid < kRem) r = src[kFull * 1024u + tid];
+  for (uint32_t i = 0; i < I::kFull; ++i) im.t[i] = src[tid + i * 1024u];
+  im.r = make_uint4(0, 0, 0, 0);
+  if (I::kRem != 0 && tid < I::kRem) im.r = src[I::kFull * 1024u + tid];
+}
+template <uint32_t kBytes>
+__device__ __forceinline__ void store_lds_image(const ImageRegs<kBytes> &im, uint4 *dst) {
+  using I = ImageRegs<kBytes>;
+  const uint32_t tid = threadIdx.x;
 #pragma unroll
-  for (uint32_t i = 0; i < kFull; ++i) dst[tid + i * 1024u] = t[i];
-  if (kRem != 0 && tid < kRem) dst[kFull * 1024u + tid] = r;
+  for (uint32_t i = 0; i < I::kFull; ++i) dst[tid + i * 1024u] = im.t[i];
+  if (I::kRem != 0 && tid < I::kRem) dst[I::kFull * 1024u + tid] = im.r;
 }
 
 // Read-only kernel inputs through the constant address space: uniform indices
@@ -443,7 +453,7 @@ struct QuarterInfo {
 // times, tools/probe.py --mode timeline.)  Finished CRCs go to an LDS ring of
 // kDynSlots rounds; the wave completing a round stores its 32 CRCs as one
 // whole 128-B line.
-constexpr uint32_t kDynRound = 32;
+// kDynRound / dyn_round(QB): crc32_kernels.h (the host sizes launches with them).
 // Rounds the LDS output ring holds: a wave that finishes a task of round r
 // waits until round r - kDynSlots has been stored.  8 (was 4): C2 -1.0 %, NS
 // -0.25 % (profiles/r02/r02bx_dyn_slots_ab.txt); the QB = 4 ring then takes
@@ -471,6 +481,11 @@ constexpr uint32_t dyn_slots(int QB) { return QB == 1 ? RPCCRC_DYN_SLOTS_QB1 : R
 #define RPCCRC_META_REUSE 1
 #endif
 constexpr bool kRowsMetaReuse = RPCCRC_META_REUSE != 0;
+// First row's loads issued under the LDS image copy (crc32_rows_kernel kEarly).
+#ifndef RPCCRC_EARLY_ROW
+#define RPCCRC_EARLY_ROW 0
+#endif
+constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
 #ifndef RPCCRC_STEAL_EXIT_ACQREL
 #define RPCCRC_STEAL_EXIT_ACQREL 0
 #endif
@@ -489,7 +504,7 @@ constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, t
 // silently (VERDICT / ADVICE r02), and no wait can turn into a hang.
 constexpr uint32_t kStealSpinMax = 1u << 21;
 constexpr uint32_t kRingSpinMax = 1u << 21;
-constexpr uint32_t dyn_ring_words(int QB) { return 1 + 2 * dyn_slots(QB) + dyn_slots(QB) * kDynRound * (uint32_t)QB; }
+constexpr uint32_t dyn_ring_words(int QB) { return 1 + 2 * dyn_slots(QB) + dyn_slots(QB) * dyn_round(QB) * (uint32_t)QB; }
 constexpr uint32_t dyn_ctl_words(int QB) { return dyn_ring_words(QB) + kStealCtlWords; }
 
 template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool DYN = false, bool STEAL = false>
@@ -497,14 +512,20 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   using namespace rows;
   static_assert(!DYN || DEPTH == 1, "DYN: DEPTH = 1");
   static_assert(!STEAL || DYN, "stealing: DYN launches");
+  constexpr uint32_t kRound = dyn_round(QB); // tasks per dealing round
   constexpr uint32_t kDynSlots = dyn_slots(QB);
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
   // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
   // rounds (generation), then the CRC ring (QB CRCs per task).
   __shared__ uint32_t s_ctl[DYN ? (STEAL ? dyn_ctl_words(QB) : dyn_ring_words(QB)) : 1];
+  // kEarlyRow: each wave's first task is static (DYN: counter index = wave, so
+  // the LDS counter starts at 16), and its first row's loads are issued between
+  // the image's global loads and its LDS stores -- the row's HBM latency then
+  // overlaps the image copy instead of following the barrier.
+  constexpr bool kEarly = kEarlyRow && (ABL & kRowsAblTimes) == 0;
   if constexpr (DYN) {
     if (threadIdx.x <= 2 * kDynSlots)
-      s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots : 0u;
+      s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots : (kEarly ? 16u : 0u);
     if (STEAL && threadIdx.x < 3 + kStealQ) s_ctl[dyn_ring_words(QB) + threadIdx.x] = 0u; // tail/done/inflight/tags
   }
   // Device-side item counts (split lists, big-body chunks) may be 0: leave
@@ -515,10 +536,18 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   // All of this thread's image loads in flight at once (a rolled loop would
   // pay one L2 round trip per 16 KiB before the first HBM byte is read).
-  if constexpr ((ABL & kRowsAblNoImage) == 0)
-    copy_lds_image<kLdsBytesV2>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
-  __syncthreads();
-  if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();
+  ImageRegs<kLdsBytesV2> img;
+  if constexpr ((ABL & kRowsAblNoImage) == 0) load_lds_image<kLdsBytesV2>(a.lds_image, img);
+  // LDS stores of the image + the barrier (kEarly: after the first row's loads
+  // are issued; the loads above were issued first, so waiting for them does
+  // not wait for the row).
+  auto image_ready = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((ABL & kRowsAblNoImage) == 0) store_lds_image<kLdsBytesV2>(img, reinterpret_cast<uint4 *>(s_lds));
+    __syncthreads();
+    if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();
+  };
+  if constexpr (!kEarly) image_ready();
   const uint8_t *lds = reinterpret_cast<const uint8_t *>(s_lds);
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -578,12 +607,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if (lane == 0) c = __hip_atomic_fetch_add(&s_ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return c;
   };
-  auto dyn_task = [&](uint32_t c) -> uint32_t { return (((c / kDynRound) * nblk + vb) * kDynRound) | (c % kDynRound); };
+  auto dyn_task = [&](uint32_t c) -> uint32_t { return (((c / kRound) * nblk + vb) * kRound) | (c % kRound); };
   // ---- tail stealing (see kStealAhead) ----
   const uint32_t steal_s = STEAL ? a.steal_s : 0u; // static local rounds per workgroup
   constexpr bool steal = STEAL;
   const uint32_t pool_first = steal_s * nblk; // first pool (global) round
-  const uint32_t pool_n = steal ? (n_tasks + kDynRound - 1) / kDynRound - pool_first : 0u;
+  const uint32_t pool_n = steal ? (n_tasks + kRound - 1) / kRound - pool_first : 0u;
   uint32_t *q_ctl = s_ctl + (STEAL ? dyn_ring_words(QB) : 0u);
   uint32_t *q_tail = q_ctl, *q_done = q_ctl + 1, *q_inflight = q_ctl + 2;
   uint32_t *q_tag = q_ctl + 3, *q_id = q_ctl + 3 + kStealQ;
@@ -626,7 +655,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // The wave taking local round r's first task claims a pool round for the
   // workgroup (for use kStealAhead rounds later).
   auto claim_if_first = [&](uint32_t c) { // uniform
-    if (!steal || c % kDynRound != 0u || c / kDynRound + kStealAhead < steal_s) return;
+    if (!steal || c % kRound != 0u || c / kRound + kStealAhead < steal_s) return;
     publish(); // at most one claim in flight per wave
     uint32_t go = 0;
     if (lane == 0 && lds_ld_acq(q_done) == 0u) {
@@ -643,7 +672,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // Counter index -> global task.  more = false: the workgroup has no work left
   // (returns n_tasks).  Static rounds as dyn_task; pool rounds from the queue.
   auto dyn_map = [&](uint32_t c, bool &more) -> uint32_t {
-    const uint32_t r = c / kDynRound;
+    const uint32_t r = c / kRound;
     more = true;
     if (!steal || r < steal_s) return dyn_task(c);
     const uint32_t q = r - steal_s, k = q % kStealQ;
@@ -663,7 +692,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (st == 1u) id = q_id[k];
       }
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
-      if (st == 1u) return ((pool_first + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kDynRound) | (c % kDynRound);
+      if (st == 1u) return ((pool_first + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kRound) | (c % kRound);
       if (st == 2u) break;
       if (spin >= kStealSpinMax) { // never in a healthy launch: fail loudly, do not hang
         if (lane == 0) report_err(kErrStealWait);
@@ -704,13 +733,22 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   };
   uint32_t first_c = 0, first_task;
   if constexpr (DYN) {
-    first_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)dyn_grab());
+    first_c = kEarly ? wave : (uint32_t)__builtin_amdgcn_readfirstlane((int)dyn_grab());
     first_task = dyn_task(first_c);
   } else {
     first_task = task_of(0);
   }
-  if (first_task >= n_tasks) return; // (never with stealing: local round 0 is static and full)
-  claim_if_first(first_c);
+  if (first_task >= n_tasks) { // (never with stealing: local round 0 is static and full)
+    if constexpr (kEarly) image_ready(); // every wave of the workgroup reaches the barrier once
+    return;
+  }
+  // After the first row's loads are issued (kEarly), the image and the LDS
+  // control block become usable here.
+  auto begin = [&]() {
+    if constexpr (kEarly) image_ready();
+    claim_if_first(first_c);
+  };
+  if constexpr (!kEarly) begin();
 
   auto synth = [&](uint32_t key, u32x4 (&buf)[4]) {
 #pragma unroll
@@ -822,22 +860,22 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // DYN output: CRC of the task with counter index c into the LDS ring; the
     // wave completing a round stores the round's CRCs as one whole line.
     auto dyn_out = [&](uint32_t c, uint32_t tsk, uint32_t res) {
-      const uint32_t rnd = c / kDynRound, idx = c % kDynRound, slot = rnd % kDynSlots;
+      const uint32_t rnd = c / kRound, idx = c % kRound, slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots;
       uint32_t old = 0;
       publish(); // the ring wait below must not hold a claim
       if (lane == 0) {
         // the slot still holds an older round that a slow wave has not finished
         ring_wait(gen, slot, rnd);
-        ring[slot * kDynRound + idx] = res;
+        ring[slot * kRound + idx] = res;
         old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
       // the round's first global task (static rounds: from the local round)
-      const uint32_t base = steal ? tsk & ~(kDynRound - 1u) : (rnd * nblk + vb) * kDynRound;
-      const uint32_t cnt = (n_tasks - base < kDynRound) ? n_tasks - base : kDynRound;
+      const uint32_t base = steal ? tsk & ~(kRound - 1u) : (rnd * nblk + vb) * kRound;
+      const uint32_t cnt = (n_tasks - base < kRound) ? n_tasks - base : kRound;
       if (old + 1u == cnt) { // this wave completed the round
-        const uint32_t v = ring[slot * kDynRound + (lane % kDynRound)];
+        const uint32_t v = ring[slot * kRound + (lane % kRound)];
         if constexpr ((ABL & kRowsAblNoStore) == 0) {
           if (lane < cnt) store_out(a.out + oidx(base + lane), v);
         } else {
@@ -912,7 +950,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // wave's next item.  Invalid successors carry the wave's first item's
     // (in-range) metadata and load from `safe`; their results are dropped.
     uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
-    if constexpr (DYN) pend = dyn_grab();
+    // After the first row's loads: the image / barrier (kEarly), then the grab
+    // of the task after the first one.
+    auto start = [&]() {
+      if constexpr (kEarly) begin();
+      if constexpr (DYN) pend = dyn_grab();
+    };
     uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
     // more: the wave may still get work (stealing: a task past n inside a
     // pool round is skipped, not the end).  Invalid rows take one step each.
@@ -994,6 +1037,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       // (Horner across rows needs that).
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
+      start();
       bool p_ok = false; // no row pending before the first step
       uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_item = 0, p_chain = 0;
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
@@ -1038,6 +1082,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     } else if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
+      start();
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
         uint32_t m_item, m_lp;
         uint64_t m_p0;
@@ -1072,6 +1117,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       uint32_t n_r, n_len, n_z, n_nr, n_seed;
       bool n_ok, n_more;
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
+      start();
       succ(true, true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed, c_p0, c_lp,
            c_len, c_z, c_seed);
       issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
@@ -1229,8 +1275,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // DYN output (see QB = 1): the 4 CRCs of group task c into the LDS ring; the
     // wave completing a round stores its (up to) 128 CRCs as two 256-B stores.
     auto dyn_out4 = [&](uint32_t c, uint32_t tsk, const uint32_t (&v)[4]) {
-      constexpr uint32_t kW = kDynRound * 4;
-      const uint32_t rnd = (uint32_t)(c / kDynRound), idx = (uint32_t)(c % kDynRound), slot = rnd % kDynSlots;
+      constexpr uint32_t kW = kRound * 4; // CRCs per round (64 or 128)
+      const uint32_t rnd = (uint32_t)(c / kRound), idx = (uint32_t)(c % kRound), slot = rnd % kDynSlots;
       uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots + slot * kW;
       uint32_t old = 0;
       publish(); // the ring wait below must not hold a claim
@@ -1242,14 +1288,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
       // first group of the round
-      const uint32_t base = steal ? tsk & ~(kDynRound - 1u) : (rnd * nblk + vb) * kDynRound;
-      const uint32_t cnt = (ngroups - base < kDynRound) ? (uint32_t)(ngroups - base) : kDynRound;
+      const uint32_t base = steal ? tsk & ~(kRound - 1u) : (rnd * nblk + vb) * kRound;
+      const uint32_t cnt = (ngroups - base < kRound) ? (uint32_t)(ngroups - base) : kRound;
       if (old + 1u == cnt) {
         const uint32_t ibase = 4 * base;
         const uint32_t nit = (n - ibase < kW) ? (uint32_t)(n - ibase) : kW;
-        const uint32_t v0 = ring[lane], v1 = ring[64 + lane];
+        const uint32_t v0 = ring[lane];
         if (lane < nit) store_out(a.out + oidx(ibase + lane), v0);
-        if (64 + lane < nit) store_out(a.out + oidx(ibase + 64 + lane), v1);
+        if constexpr (kW > 64) {
+          const uint32_t v1 = ring[64 + lane];
+          if (64 + lane < nit) store_out(a.out + oidx(ibase + 64 + lane), v1);
+        }
         if (lane == 0) {
           done[slot] = 0;
           __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1305,6 +1354,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       QuadMeta c_qm = issue(g, true, safe, bufA);
+      if constexpr (kEarly) begin();
       uint32_t pend = 0;
       if constexpr (DYN) pend = dyn_grab();
       uint32_t c_c = first_c;
@@ -1356,6 +1406,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
+      if constexpr (kEarly) begin();
       uint32_t gn = next_task(g);
       n_qm = issue(gn < ngroups ? gn : g, gn < ngroups, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {

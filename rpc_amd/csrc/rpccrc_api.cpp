@@ -340,7 +340,7 @@ const uint32_t g_big_min = [] {
   return (v >= 16384 && v <= 0xFFFFFFFFull) ? (uint32_t)v : kBigMin;
 }();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
-constexpr uint64_t kPackedMinBodies = 64;         // fewer frames: one wave per body (rows kernel)
+constexpr uint64_t kSplitMinFrames = 16384;       // fewer frames: one wave per body (rows kernel)
 constexpr bool kAutoSplitFrames = true;           // AUTO frames batches: split (true) or packed (false)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
 // Chunks per packed slice, at least: a slice switch costs the wave two scalar
@@ -494,7 +494,7 @@ struct StealLease {
   }
   int get(const DeviceCtx &c, uint64_t n, int QB, hipStream_t stream) {
     const uint64_t tasks = QB == 4 ? (n + 3) / 4 : n;
-    if (tasks < 8ull * 32ull * (uint64_t)max_blocks_for(c)) return RPCCRC_OK;
+    if (tasks < 8ull * dyn_round(QB) * (uint64_t)max_blocks_for(c)) return RPCCRC_OK; // launch_rows: not DYN
     if (const int rc = c.steal->acquire(stream, &slot)) return rc;
     p = slot->p;
     pool = c.steal;
@@ -529,7 +529,11 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   const bool nt = nontemporal();
   const int mb = max_blocks_for(c);
   const bool fits = n < (1ull << 27); // the packed kernel's metadata window: 8-B offsets in a 1 GiB buffer range
-  const bool auto_frames = path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kPackedMinBodies;
+  // AUTO frames batches split only when they are large: the split's flag /
+  // scan / scatter passes and second rows launch cost ~20 us, which only a
+  // batch of many frames repays (1M frames: 334 vs 565 us); a
+  // small batch (e.g. 1024 lifted-cap frames) takes the rows kernel directly.
+  const bool auto_frames = path == RPCCRC_RAGGED_AUTO && small_bodies && n >= kSplitMinFrames;
   const bool packed = fits && (path == RPCCRC_RAGGED_PACKED || (auto_frames && !kAutoSplitFrames));
   const bool split = !packed && n <= kMaxLaunchItems && (path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
   route = route && !packed && mode == kModeFinal && n <= kMaxLaunchItems;

@@ -111,9 +111,18 @@ def test_frames_zero_length_bodies(lift_cap):
                  for t in (0, 1, 2, 3, 0xFFFF) for c in (0, 1, 0x80000000, 0xFFFFFFFF)]
 
 
+@pytest.fixture(params=["auto", "split"])
+def frames_path(request):
+    """AUTO frames batches below 16384 frames take the rows kernel; "split" forces the
+    split path (small bodies four per row) that large frames batches take."""
+    rpc_amd.set_ragged_path(request.param)
+    yield request.param
+    rpc_amd.set_ragged_path("auto")
+
+
 @pytest.mark.parametrize("role", ["server", "client"])
 @pytest.mark.parametrize("lift_cap", [False, True])
-def test_frames_type_rules(role, lift_cap):
+def test_frames_type_rules(role, lift_cap, frames_path):
     """Heartbeats whose crc32 / body_len fields are not zero, unknown types, over-cap
     lengths, empty bodies (one frame in eight): every verdict and CRC equals the
     reference's decision."""
@@ -185,7 +194,7 @@ def test_frames_stamp_cap_and_bounds():
         assert out[-3:] == blob[-3:]
 
 
-def test_frames_lifted_cap_large_bodies():
+def test_frames_lifted_cap_large_bodies(frames_path):
     """frames with bodies from 1 B to 64 MiB (MAX_BODY_LEN lifted), stamped
     then verified on the device; the bodies >= 256 KiB go through the chunk route."""
     rng = np.random.default_rng(11)

@@ -52,6 +52,10 @@ for s in $STEPS; do
                  -d "$OUT/pmcmix2_$c" -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive --no-live-traffic || exit 1
            done ;;
     bench_c3) run bench_c3 600 python bench.py --config c3 --no-cpu-baseline --no-host-inclusive ;;
+    tests_variant) # GPU parity of an A/B build: VARIANT=<abtest name>
+           RPCCRC_LIB=$PWD/abtest/${VARIANT}.so run tests_variant_$VARIANT 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -rfE \
+               --timeout 120 --timeout-method thread -k "dynamic or stealing or c1_ or north_star or uniform or c2_ or c4_" ;;
+    ab) run ab 1200 bash tools/ab_lib.sh "$TAG/ab" "${AB_LIBS:-head}" "${AB_CFGS:-ns}" "${AB_ROUNDS:-2}" ;;
     ablate_half) run ablate_half 600 python tools/probe.py --mode ablate --rounds 3 --config u2k \
                    --only qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl9216_d1,qb1_pair1_nt1_abl1027_d1 ;;
     prof_frames) run prof_frames 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_frames" -o run --output-format csv -- \

@@ -40,7 +40,7 @@ void go(const ItemsArgs &a, int blocks, hipStream_t s) {
     }
     ItemsArgs k = a;
     const uint64_t tasks = QB == 4 ? (a.n_items + 3) / 4 : a.n_items;
-    const uint64_t rounds = (tasks + kDynRound - 1) / kDynRound;
+    const uint64_t rounds = (tasks + dyn_round(QB) - 1) / dyn_round(QB);
     const uint64_t st = (uint64_t)((double)rounds * 0.85) / (uint64_t)blocks;
     k.steal = g_steal;
     k.steal_s = (uint32_t)st;
