@@ -38,7 +38,8 @@ struct ItemsArgs {
   // last workgroup (crc32_rows.h kStealAhead).  nullptr: static rounds only.
   // steal_s is set by launch_rows.
   uint32_t *steal = nullptr;
-  uint32_t steal_s = 0;
+  uint32_t steal_s = 0;         // kStealOnDevice: the kernel sizes the pool from the device count
+  uint32_t steal_permille = 150; // pool share of the rounds (steal_s on the device)
   // Words zeroed by workgroup 0 at launch (<= 1024; the contiguous chunk
   // combine XORs into them afterwards).
   uint32_t *zero_out = nullptr;
@@ -53,6 +54,8 @@ struct ItemsArgs {
   uint32_t test_giveup = 0;
 };
 
+constexpr uint32_t kStealOnDevice = 0xFFFFFFFFu; // ItemsArgs.steal_s: computed in the kernel (device-counted n)
+
 // Device error bits (ItemsArgs.err).
 constexpr uint32_t kErrStealWait = 1u; // a wave gave up waiting for a stolen round: its tasks were not run
 constexpr uint32_t kErrRingWait = 2u;  // a wave gave up waiting for an output-ring slot: CRCs may be stale
@@ -65,7 +68,11 @@ constexpr uint32_t kErrRingWait = 2u;  // a wave gave up waiting for an output-r
 constexpr uint32_t kBigMin = 256u << 10;
 constexpr uint32_t kBigMaxBodies = 16384;
 constexpr uint64_t kBigMaxChunks = 1ull << 20;
-constexpr uint64_t kBigMinChunk = 16384; // power of two; grows so the chunks fit kBigMaxChunks
+// Default first chunk size: one-row chunks (4080 B: with the body's end pad
+// z <= 15 a chunk still fits one 4 KiB row), so the chunk pass deals its tail
+// with stealing (16 KiB chunks until round 3, five rows each when z != 0).
+// The plan grows it as (chunk + 16) * 2 - 16 until the chunks fit kBigMaxChunks.
+constexpr uint64_t kBigMinChunk = 4096 - 16;
 struct BigRoute {
   uint32_t *routed;  // bit i: body i takes the route (ceil(n / 64) * 2 words, all written)
   uint64_t *meta;    // [0] bodies claimed, [1] their bytes, [2] chunks, [3] chunk bytes
@@ -74,6 +81,7 @@ struct BigRoute {
   uint64_t *c_off;   // kBigMaxChunks: chunk offsets / lengths / crc0
   uint32_t *c_len;
   uint32_t *c_raw;
+  uint64_t min_chunk = kBigMinChunk; // the plan's starting chunk size (power of two)
 };
 size_t big_route_workspace_bytes(uint64_t n);
 BigRoute big_route_carve(void *ws, uint64_t n);
@@ -84,8 +92,12 @@ hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big
                                hipStream_t s);
 // After the rows pass: chunk plan, chunk CRCs (rows kernel, RAW), per-body
 // fold into out[batch index].
+// steal: a leased zeroed two-word counter for the chunk pass's tail stealing
+// (nullptr: static rounds); its event is recorded as the chunk pass's
+// completion (steal_done, *steal_recorded) like launch_rows.
 hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,
-                            hipStream_t s);
+                            hipStream_t s, uint32_t *steal = nullptr, hipEvent_t steal_done = nullptr,
+                            bool *steal_recorded = nullptr);
 
 constexpr uint32_t kShiftNibWords = 64u * 8u * 16u; // 32 KiB: the chunk combine's shift maps
 

@@ -267,10 +267,13 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // rounds go to the device-counter pool, the rest stay static per workgroup.
   ItemsArgs k = a;
   k.steal_s = 0;
+  k.steal_permille = (uint32_t)(steal_frac() * 1000.0 + 0.5);
   if (dyn && a.steal != nullptr && a.n_dev == nullptr) {
     const uint64_t rounds = (n_tasks + round - 1) / round;
     const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac())) / blocks;
     if (st >= kStealAhead && st * blocks < rounds) k.steal_s = (uint32_t)st;
+  } else if (dyn && a.steal != nullptr && k.steal_permille > 0) {
+    k.steal_s = kStealOnDevice; // device-counted: the kernel sizes the pool from *n_dev
   }
   if (k.steal_s == 0) k.steal = nullptr;
 #define RPCCRC_ROWS(Q, N, R)                                                                      \
@@ -586,12 +589,15 @@ __global__ void __launch_bounds__(1024) big_plan_kernel(const uint32_t *lengths,
   if (nb == 0) {
     if (t == 0) {
       r.meta[2] = 0;
-      r.meta[3] = kBigMinChunk;
+      r.meta[3] = r.min_chunk;
     }
     return;
   }
-  uint64_t chunk = kBigMinChunk; // sum ceil(len / chunk) <= bytes / chunk + 1 + nb
-  while (r.meta[1] / chunk + 1 + nb > kBigMaxChunks) chunk <<= 1;
+  // Chunks of (2^k) * 4096 - 16 bytes: end-aligned chunks all share their body's
+  // end pad z < 16, so each takes exactly 2^k rows (a 4096-byte chunk with
+  // z != 0 would take two).  sum ceil(len / chunk) <= bytes / chunk + 1 + nb
+  uint64_t chunk = r.min_chunk;
+  while (r.meta[1] / chunk + 1 + nb > kBigMaxChunks) chunk = ((chunk + 16) << 1) - 16;
   if (t == 0) run = 0;
   __syncthreads();
   for (uint64_t base = 0; base < nb; base += 1024) {
@@ -637,13 +643,21 @@ __global__ void __launch_bounds__(256) big_expand_kernel(const uint64_t *offsets
 }
 
 // Persistent fold: block b takes routed bodies b, b + grid, ...: thread t runs
-// Horner over chunks t, t + 1024, ... with the step map A_{1024 * chunk} (one
-// nibble map: chunk is a power of two), shifts its partial to the body end,
-// and the block XOR-reduces: crc = ~(A_L(F) ^ XOR_k A_{(nch-1-k) chunk}(raw_k)).
+// Horner over chunks t, t + 1024, ... with the step map A_{1024 * chunk} (built
+// once per block as one nibble table: the chunk is 2^k * 4096 - 16 bytes, not a
+// power of two), shifts its partial to the body end, and the block
+// XOR-reduces: crc = ~(A_L(F) ^ XOR_k A_{(nch-1-k) chunk}(raw_k)).
+__device__ __forceinline__ uint32_t nib_map(const uint32_t *m, uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) r ^= m[i * 16u + ((v >> (4u * i)) & 15u)];
+  return r;
+}
 __global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengths, BigRoute r, const uint4 *shift_nib,
                                                            uint32_t *out) {
   __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
   __shared__ uint32_t part[16];
+  __shared__ uint32_t stepnib[128]; // [i][j] = A_{1024 * chunk}(j << 4i)
   const uint64_t nb = big_count(r);
   if (blockIdx.x >= nb) return;
   const uint32_t t = threadIdx.x;
@@ -654,11 +668,13 @@ __global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengt
   }
   __syncthreads();
   const uint64_t chunk = r.meta[3], step = 1024ull * chunk;
+  if (t < 128) stepnib[t] = nib_shift(nib, step, (t & 15u) << (4u * (t >> 4)));
+  __syncthreads();
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint32_t i = r.b_idx[b];
     const uint64_t L = lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first;
     uint32_t acc = 0;
-    for (uint64_t k = t; k < nch; k += 1024) acc = nib_shift(nib, step, acc) ^ r.c_raw[first + k];
+    for (uint64_t k = t; k < nch; k += 1024) acc = nib_map(stepnib, acc) ^ r.c_raw[first + k];
     if (t < nch) {
       const uint64_t kl = t + (nch - 1 - t) / 1024 * 1024;
       acc = nib_shift(nib, (nch - 1 - kl) * chunk, acc);
@@ -710,7 +726,7 @@ hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big
 }
 
 hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,
-                            hipStream_t s) {
+                            hipStream_t s, uint32_t *steal, hipEvent_t steal_done, bool *steal_recorded) {
   if (proto.n_items == 0) return hipSuccess;
   if (proto.mode != kModeFinal || proto.offsets == nullptr || proto.lengths == nullptr) return hipErrorInvalidValue;
   hipLaunchKernelGGL(big_plan_kernel, dim3(1), dim3(1024), 0, s, proto.lengths, r);
@@ -729,7 +745,10 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
   a.big_min = 0xFFFFFFFFu;
   a.mode = kModeRaw;
   a.out = r.c_raw;
-  e = launch_rows(a, 1, nt, max_blocks, s);
+  // One-row chunks (4080 B): the tail is dealt from the steal counter, the
+  // pool sized in the kernel from the device count (crc32_rows.h steal_s).
+  a.steal = steal;
+  e = launch_rows(a, 1, nt, max_blocks, s, steal_done, steal_recorded);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(big_combine_kernel, dim3(256), dim3(1024), 0, s, proto.lengths, r, shift_nib, proto.out);
   return hipGetLastError();

@@ -525,7 +525,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   constexpr bool kEarly = kEarlyRow && (ABL & kRowsAblTimes) == 0;
   if constexpr (DYN) {
     if (threadIdx.x <= 2 * kDynSlots)
-      s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots : (kEarly ? 16u : 0u);
+      s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots
+                                                      : ((threadIdx.x == 0u && kEarly) ? 16u : 0u);
     if (STEAL && threadIdx.x < 3 + kStealQ) s_ctl[dyn_ring_words(QB) + threadIdx.x] = 0u; // tail/done/inflight/tags
   }
   // Device-side item counts (split lists, big-body chunks) may be 0: leave
@@ -609,8 +610,18 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   };
   auto dyn_task = [&](uint32_t c) -> uint32_t { return (((c / kRound) * nblk + vb) * kRound) | (c % kRound); };
   // ---- tail stealing (see kStealAhead) ----
-  const uint32_t steal_s = STEAL ? a.steal_s : 0u; // static local rounds per workgroup
-  constexpr bool steal = STEAL;
+  // Static local rounds per workgroup.  Device-counted launches (a.n_dev: the
+  // big-body route's chunk pass) size the pool here, as launch_rows does on
+  // the host; too few rounds -> no pool (then `steal` is false and the
+  // STEAL instantiation deals like plain DYN).
+  const uint32_t steal_s = [&]() -> uint32_t {
+    if constexpr (!STEAL) return 0u;
+    if (a.steal_s != kStealOnDevice) return a.steal_s;
+    const uint32_t rounds = (n_tasks + kRound - 1) / kRound;
+    const uint32_t st = (uint32_t)(((uint64_t)rounds * (1000u - a.steal_permille)) / 1000u) / nblk;
+    return (st >= kStealAhead && st * nblk < rounds) ? st : 0u;
+  }();
+  const bool steal = STEAL && steal_s != 0u;
   const uint32_t pool_first = steal_s * nblk; // first pool (global) round
   const uint32_t pool_n = steal ? (n_tasks + kRound - 1) / kRound - pool_first : 0u;
   uint32_t *q_ctl = s_ctl + (STEAL ? dyn_ring_words(QB) : 0u);
@@ -721,11 +732,15 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       const uint32_t old = __hip_atomic_fetch_add(a.steal + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
       if (old + 1u == nblk) {
-        // Only the last workgroup pays for an explicit ordering point before
-        // the reset: every other workgroup's exit increment
-        // follows its returned claims, and this fence orders the reset after
-        // the increments it has observed.
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // No fence here (ADVICE r02 asked for an acquire fence on this path).
+        // At agent scope on gfx950 that fence is an L2 invalidate, which cost
+        // every stealing launch ~30-45 us (NS 602 -> 645 us, C1 161 -> 190 us,
+        // profiles/r03/r03b_*). The fence is also unnecessary: the claims, the
+        // exit increments and this reset all touch the same two words as
+        // agent-scope atomics, so they are performed at one coherence point.
+        // Each workgroup's increment is issued after its claims have returned,
+        // and this store is issued after the increment that returned nblk - 1,
+        // so it lands after every claim of the launch.
         __hip_atomic_store(a.steal, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.steal + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

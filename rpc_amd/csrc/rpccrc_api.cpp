@@ -334,10 +334,30 @@ const uint64_t g_large_chunk = [] {
 const bool g_large_chunk_env = getenv("RPCCRC_LARGE_CHUNK") != nullptr;
 // Ragged bodies of at least this many bytes take the on-device chunk route
 // (DESIGN.md 4.6).  Tuning override: RPCCRC_BIG_MIN (bytes, >= 16 KiB).
-const uint32_t g_big_min = [] {
+const uint32_t g_big_min_env = [] {
   const char *e = getenv("RPCCRC_BIG_MIN");
   const unsigned long long v = e ? strtoull(e, nullptr, 10) : 0ull;
-  return (v >= 16384 && v <= 0xFFFFFFFFull) ? (uint32_t)v : kBigMin;
+  return (v >= 16384 && v <= 0xFFFFFFFFull) ? (uint32_t)v : 0u;
+}();
+// A batch that the route can hold whole (n <= kBigMaxBodies) has too few
+// bodies to keep the chip busy with one wave per body: a 255 KiB body was one
+// wave's 64-row walk, 87 us of the 1024 lifted-cap frames' 760 us
+// (profiles/r03/r03b_frames_kernel_stats.csv).  Such batches route every body
+// of >= 16 KiB (at most 4 rows stay on one wave); large batches keep 256 KiB.
+constexpr uint32_t kBigMinSmallBatch = 16384;
+uint32_t big_min_for(uint64_t n) {
+  if (g_big_min_env) return g_big_min_env;
+  return n <= kBigMaxBodies ? kBigMinSmallBatch : kBigMin;
+}
+// Chunk size the route starts from (it grows as (c + 16) * 2 - 16 until the
+// chunks fit kBigMaxChunks): 4080-byte one-row chunks deal with tail stealing
+// (launch_rows, device-counted).  Tuning override: RPCCRC_BIG_CHUNK
+// (2^k * 4096 - 16 bytes, e.g. 16368).
+const uint32_t g_big_chunk = [] {
+  const char *e = getenv("RPCCRC_BIG_CHUNK");
+  const unsigned long long v = e ? strtoull(e, nullptr, 10) : 0ull;
+  const unsigned long long p = v + 16;
+  return (v >= kBigMinChunk && p <= (1ull << 30) && (p & (p - 1)) == 0) ? (uint32_t)v : (uint32_t)kBigMinChunk;
 }();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kSplitMinFrames = 16384;       // fewer frames: one wave per body (rows kernel)
@@ -567,18 +587,25 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   if (split_bytes + route_bytes > 0)
     if (const int rc = ws.get(c.ws, split_bytes + route_bytes, s)) return rc;
   BigRoute r{};
+  StealLease sl; // the route's chunk pass deals its tail from this counter (device-counted)
   if (route) {
+    const uint32_t big_min = big_min_for(n);
     r = big_route_carve(ws.ptr() + split_bytes, n);
-    RPCCRC_TRY(launch_big_classify(lengths, n, g_big_min, r, s));
+    r.min_chunk = g_big_chunk;
+    RPCCRC_TRY(launch_big_classify(lengths, n, big_min, r, s));
     a.routed = r.routed;
-    a.big_min = g_big_min;
+    a.big_min = big_min;
+    if (const int rc = c.steal->acquire(s, &sl.slot)) return rc;
+    sl.p = sl.slot->p;
+    sl.pool = c.steal;
+    sl.s = s;
   }
   if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
   } else {
     RPCCRC_TRY(launch_rows(a, 1, nt, mb, s));
   }
-  if (route) RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s));
+  if (route) RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s, sl.p, sl.done_event(), &sl.recorded));
   return RPCCRC_OK;
 }
 
@@ -1047,7 +1074,7 @@ int rpc_crc32_device_batch_bounded(const uint8_t *d_base, const uint64_t *d_offs
   // fold after it: ~30 us of launches, profiles/r02final4/c2_kernel_stats.csv)
   // are not launched.  A body over a wrong bound is still CRC'd correctly by
   // the rows pass (one wave for the whole body): the hint is about speed only.
-  const bool route = max_len == 0 || max_len >= g_big_min;
+  const bool route = max_len == 0 || max_len >= big_min_for(n);
   return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream), false, route);
 }
 
