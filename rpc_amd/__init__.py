@@ -176,6 +176,10 @@ def device_batch(base, offsets, lengths, out=None, stream=None, max_len: int = 0
     if lengths.numel() != n:
         raise ValueError("offsets and lengths differ in length")
     out = _dev_u32_out(n, base.device, out)
+    if _lib.rpc_crc32_device_batch_bounded is None:  # an older build under A/B (tools/ab_lib.sh)
+        check(_lib.rpc_crc32_device_batch(base.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), n,
+                                          out.data_ptr(), _stream_handle(stream)), "rpc_crc32_device_batch")
+        return out
     check(_lib.rpc_crc32_device_batch_bounded(base.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), n,
                                               int(max_len) & 0xFFFFFFFF, out.data_ptr(), _stream_handle(stream)),
           "rpc_crc32_device_batch_bounded")

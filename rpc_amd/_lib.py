@@ -39,7 +39,15 @@ _sz = ctypes.c_size_t
 
 
 def _sig(name, restype, *argtypes):
-    f = getattr(lib, name)
+    try:
+        f = getattr(lib, name)
+    except AttributeError:
+        # A/B runs may point RPCCRC_LIB at an older build (tools/ab_lib.sh) that
+        # lacks a newer entry point; the in-tree library must export them all
+        # (tests/test_abi.py).
+        if "RPCCRC_LIB" in os.environ:
+            return None
+        raise
     f.restype = restype
     f.argtypes = list(argtypes)
     return f

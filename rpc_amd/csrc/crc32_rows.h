@@ -252,27 +252,17 @@ __device__ __forceinline__ uint32_t swap_lanebit4(uint32_t v, bool upper) {
 // stays in a register (a conditionally written local array went to scratch:
 // 176 B per lane, the image loaded twice).
 template <uint32_t kBytes>
-struct ImageRegs {
-  static constexpr uint32_t kN16 = kBytes / 16, kFull = kN16 / 1024, kRem = kN16 % 1024;
+__device__ __forceinline__ void copy_lds_image(const uint4 *src, uint4 *dst) {
+  constexpr uint32_t kN16 = kBytes / 16, kFull = kN16 / 1024, kRem = kN16 % 1024;
+  const uint32_t tid = threadIdx.x;
   uint4 t[kFull];
-  uint4 r;
-};
-template <uint32_t kBytes>
-__device__ __forceinline__ void load_lds_image(const uint4 *src, ImageRegs<kBytes> &im) {
-  using I = ImageRegs<kBytes>;
-  const uint32_t tid = threadIdx.x;
 #pragma unroll
-  for (uint32_t i = 0; i < I::kFull; ++i) im.t[i] = src[tid + i * 1024u];
-  im.r = make_uint4(0, 0, 0, 0);
-  if (I::kRem != 0 && tid < I::kRem) im.r = src[I::kFull * 1024u + tid];
-}
-template <uint32_t kBytes>
-__device__ __forceinline__ void store_lds_image(const ImageRegs<kBytes> &im, uint4 *dst) {
-  using I = ImageRegs<kBytes>;
-  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = 0; i < kFull; ++i) t[i] = src[tid + i * 1024u];
+  uint4 r = make_uint4(0, 0, 0, 0);
+  if (kRem != 0 && tid < kRem) r = src[kFull * 1024u + tid];
 #pragma unroll
-  for (uint32_t i = 0; i < I::kFull; ++i) dst[tid + i * 1024u] = im.t[i];
-  if (I::kRem != 0 && tid < I::kRem) dst[I::kFull * 1024u + tid] = im.r;
+  for (uint32_t i = 0; i < kFull; ++i) dst[tid + i * 1024u] = t[i];
+  if (kRem != 0 && tid < kRem) dst[kFull * 1024u + tid] = r;
 }
 
 // Read-only kernel inputs through the constant address space: uniform indices
@@ -537,18 +527,41 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   // All of this thread's image loads in flight at once (a rolled loop would
   // pay one L2 round trip per 16 KiB before the first HBM byte is read).
-  ImageRegs<kLdsBytesV2> img;
-  if constexpr ((ABL & kRowsAblNoImage) == 0) load_lds_image<kLdsBytesV2>(a.lds_image, img);
-  // LDS stores of the image + the barrier (kEarly: after the first row's loads
-  // are issued; the loads above were issued first, so waiting for them does
-  // not wait for the row).
-  auto image_ready = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((ABL & kRowsAblNoImage) == 0) store_lds_image<kLdsBytesV2>(img, reinterpret_cast<uint4 *>(s_lds));
+  constexpr uint32_t kImgFull = kLdsBytesV2 / 16 / 1024, kImgRem = (kLdsBytesV2 / 16) % 1024;
+  // kEarly: the image in registers until the first row's loads are issued
+  // (native vectors: HIP's uint4 struct copies became memcpys through a
+  // private-memory array -- 160 B of scratch per lane).
+  using img_v = unsigned int __attribute__((ext_vector_type(4)));
+  const img_v *img_src = reinterpret_cast<const img_v *>(a.lds_image);
+  img_v *img_dst = reinterpret_cast<img_v *>(s_lds);
+  img_v img_t[kEarly ? kImgFull : 1];
+  img_v img_r = img_v{0u, 0u, 0u, 0u};
+  if constexpr (!kEarly) {
+    if constexpr ((ABL & kRowsAblNoImage) == 0) copy_lds_image<kLdsBytesV2>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
     __syncthreads();
     if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();
-  };
-  if constexpr (!kEarly) image_ready();
+  } else if constexpr ((ABL & kRowsAblNoImage) == 0) {
+#pragma unroll
+    for (uint32_t i = 0; i < kImgFull; ++i) img_t[i] = img_src[threadIdx.x + i * 1024u];
+    if (kImgRem != 0 && threadIdx.x < kImgRem) img_r = img_src[kImgFull * 1024u + threadIdx.x];
+  }
+  // LDS stores of the image + the barrier (kEarly: after the first row's loads
+  // are issued; the loads above were issued first, so waiting for them does
+  // not wait for the row).  A macro, not a lambda: a lambda capturing `img` by
+  // reference kept it in memory -- 160 B of scratch per lane, the image
+  // round-tripped through HBM on every launch (+70 MB per launch, NS 602 ->
+  // 645 us; -Rpass-analysis=kernel-resource-usage).
+#define RPCCRC_ROWS_IMAGE_READY()                                                                          \
+  do {                                                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                                                     \
+    if constexpr ((ABL & kRowsAblNoImage) == 0) {                                                          \
+      _Pragma("unroll") for (uint32_t i = 0; i < kImgFull; ++i) img_dst[threadIdx.x + i * 1024u] = img_t[i]; \
+      if (kImgRem != 0 && threadIdx.x < kImgRem) img_dst[kImgFull * 1024u + threadIdx.x] = img_r;           \
+    }                                                                                                      \
+    __syncthreads();                                                                                       \
+    if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();                  \
+  } while (0)
+  // (!kEarly: the image is in LDS already, above)
   const uint8_t *lds = reinterpret_cast<const uint8_t *>(s_lds);
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -733,9 +746,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 #endif
       if (old + 1u == nblk) {
         // No fence here (ADVICE r02 asked for an acquire fence on this path).
-        // At agent scope on gfx950 that fence is an L2 invalidate, which cost
-        // every stealing launch ~30-45 us (NS 602 -> 645 us, C1 161 -> 190 us,
-        // profiles/r03/r03b_*). The fence is also unnecessary: the claims, the
+        // At agent scope on gfx950 that fence is an L2 invalidate. It is not
+        // needed for the reset to be ordered: the claims, the
         // exit increments and this reset all touch the same two words as
         // agent-scope atomics, so they are performed at one coherence point.
         // Each workgroup's increment is issued after its claims have returned,
@@ -754,16 +766,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     first_task = task_of(0);
   }
   if (first_task >= n_tasks) { // (never with stealing: local round 0 is static and full)
-    if constexpr (kEarly) image_ready(); // every wave of the workgroup reaches the barrier once
+    if constexpr (kEarly) RPCCRC_ROWS_IMAGE_READY(); // every wave of the workgroup reaches the barrier once
     return;
   }
   // After the first row's loads are issued (kEarly), the image and the LDS
-  // control block become usable here.
-  auto begin = [&]() {
-    if constexpr (kEarly) image_ready();
-    claim_if_first(first_c);
-  };
-  if constexpr (!kEarly) begin();
+  // control block become usable: RPCCRC_ROWS_BEGIN() at each first issue.
+#define RPCCRC_ROWS_BEGIN()                             \
+  do {                                                  \
+    if constexpr (kEarly) RPCCRC_ROWS_IMAGE_READY();    \
+    claim_if_first(first_c);                            \
+  } while (0)
+  if constexpr (!kEarly) RPCCRC_ROWS_BEGIN();
 
   auto synth = [&](uint32_t key, u32x4 (&buf)[4]) {
 #pragma unroll
@@ -967,10 +980,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
     // After the first row's loads: the image / barrier (kEarly), then the grab
     // of the task after the first one.
-    auto start = [&]() {
-      if constexpr (kEarly) begin();
-      if constexpr (DYN) pend = dyn_grab();
-    };
+#define RPCCRC_ROWS_START()                        \
+  do {                                             \
+    if constexpr (kEarly) RPCCRC_ROWS_BEGIN();     \
+    if constexpr (DYN) pend = dyn_grab();          \
+  } while (0)
     uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
     // more: the wave may still get work (stealing: a task past n inside a
     // pool round is skipped, not the end).  Invalid rows take one step each.
@@ -1052,7 +1066,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       // (Horner across rows needs that).
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      start();
+      RPCCRC_ROWS_START();
       bool p_ok = false; // no row pending before the first step
       uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_item = 0, p_chain = 0;
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
@@ -1097,7 +1111,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     } else if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      start();
+      RPCCRC_ROWS_START();
       auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
         uint32_t m_item, m_lp;
         uint64_t m_p0;
@@ -1132,7 +1146,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       uint32_t n_r, n_len, n_z, n_nr, n_seed;
       bool n_ok, n_more;
       issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      start();
+      RPCCRC_ROWS_START();
       succ(true, true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed, c_p0, c_lp,
            c_len, c_z, c_seed);
       issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
@@ -1369,7 +1383,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if constexpr (DEPTH == 1) {
       u32x4 bufA[4], bufB[4];
       QuadMeta c_qm = issue(g, true, safe, bufA);
-      if constexpr (kEarly) begin();
+      if constexpr (kEarly) RPCCRC_ROWS_BEGIN();
       uint32_t pend = 0;
       if constexpr (DYN) pend = dyn_grab();
       uint32_t c_c = first_c;
@@ -1421,7 +1435,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
-      if constexpr (kEarly) begin();
+      if constexpr (kEarly) RPCCRC_ROWS_BEGIN();
       uint32_t gn = next_task(g);
       n_qm = issue(gn < ngroups ? gn : g, gn < ngroups, safe, bufB);
       auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) -> bool {
@@ -1455,6 +1469,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     }
   }
   steal_exit();
+#undef RPCCRC_ROWS_START
+#undef RPCCRC_ROWS_BEGIN
+#undef RPCCRC_ROWS_IMAGE_READY
 }
 
 } // namespace rpccrc
