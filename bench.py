@@ -517,8 +517,10 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
     if os.environ.get("RPCCRC_BENCH_LAUNCH_ONLY"):  # CPU rehearsal of the launch path (tests/test_bench_launch.py)
-        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus,
-                          "master": os.environ.get("MASTER_ADDR"), "config": args.config}), flush=True)
+        line = json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus,
+                           "master": os.environ.get("MASTER_ADDR"), "config": args.config}) + "\n"
+        sys.stdout.flush()
+        os.write(1, line.encode())  # one write(2) < PIPE_BUF: ranks sharing the pipe cannot interleave
         return
     _load_gpu_modules()
     from rpc_amd.shard import barrier, max_over_ranks, sum_over_ranks

@@ -60,7 +60,20 @@ constexpr uint32_t kLdsTQ16 = kLdsZI2 + 15 * 512; // 157696
 constexpr uint32_t kLdsZero = kLdsTQ16 + 1028;
 static_assert(kLdsTQ16 + 1040 == kLdsBytesV2, "rows image size");
 static_assert(kLdsBytesV2 % 16 == 0 && kLdsBytesV2 <= 163840, "fits the 160 KiB LDS");
-void build_lds_image_v2(uint32_t *img /* kLdsBytesV2 bytes */);
+// ---- sub-row shifts (ragged QB = 1 kernels only: image V3 = V2 + pad + SQ) ----
+//   SQ  2 KiB   SQ(j, n, nib) = A_{16*(3-j)}(nib << 4n), j = 0..3, at byte
+//               kLdsSQ + n*256 + j*64 + nib*4.  A first row of <= 1 KiB ("quarter
+//               row") shifts lane L's 16-B piece by A_{16*(3-(L>>4))}; a first
+//               row of <= 2 KiB ("half row") shifts the first 32-B half of each
+//               64-B segment by A_32 (j = 1).  Bank = 16*(j&1) + nib: the lanes
+//               of one half-wave (j in {0,1} or {2,3}) never collide, lanes with
+//               equal (j, nib) read one word (broadcast).  256-B aligned so one
+//               v_perm_b32 forms {j*64 + nib*4 | base}; n rides in the immediate.
+constexpr uint32_t kLdsSQ = (kLdsBytesV2 + 255u) & ~255u; // 158976
+constexpr uint32_t kLdsBytesV3 = kLdsSQ + 2048u;         // 161024
+static_assert(kLdsBytesV3 % 16 == 0 && kLdsBytesV3 <= 163840, "fits the 160 KiB LDS");
+constexpr uint32_t sq_byte(uint32_t j, uint32_t n, uint32_t nib) { return kLdsSQ + n * 256u + j * 64u + nib * 4u; }
+void build_lds_image_v2(uint32_t *img /* kLdsBytesV3 bytes: V2 + the SQ tables */);
 
 // Host-side builder (crc32_tables.cpp).
 void build_tq(uint32_t *tq /* kTqEntries */);

@@ -351,6 +351,11 @@ constexpr int kRowsAblHalfChain = 8192;
 #define RPCCRC_ROWS_PIPE 1
 #endif
 constexpr bool kRowsPipe = RPCCRC_ROWS_PIPE != 0;
+// Ragged QB = 1: first rows of <= 1 / 2 KiB as quarter / half rows (rows::sub_chain).
+#ifndef RPCCRC_SUBROWS
+#define RPCCRC_SUBROWS 1
+#endif
+constexpr bool kSubRows = RPCCRC_SUBROWS != 0;
 
 namespace rows {
 
@@ -416,6 +421,68 @@ __device__ __forceinline__ RowMerge merge_row(const uint8_t *lds, uint32_t v, ui
   m.crc = (uint32_t)__builtin_amdgcn_readlane((int)t, 4);
   m.rwu = (uint32_t)__builtin_amdgcn_readlane((int)t, 12);
   return m;
+}
+
+// ---- sub-row first rows (ragged QB = 1; crc32_layout.h SQ) ----
+// A body's first row holds its first hd <= 4096 bytes (end-aligned rows), so
+// a first row of hd <= 1 KiB has data in load 3 only, and one of hd <= 2 KiB in
+// loads 2 and 3; the pieces before the body read as zeros (out of range).  The
+// full row spends 16 chain steps per lane on them anyway.  These variants
+// spread the live bytes over all 64 lanes instead (4 or 8 chain steps), shift
+// the pieces to their 64-B segment's end with one per-lane SQ lookup pass,
+// and leave the full-row layout (lane L' = crc0 of 64-B segment L', zero for
+// the empty segments), so merge_lo / merge_row are shared.  C2: 2.15M of its
+// 12.47M rows are quarter rows and 0.85M half rows.
+// s -> A_{16*(3-j)}(s), jb = (j * 64) * 0x01010101 (this lane's j):
+// 8 lookups, each address one v_perm_b32 {byte j*64 + nib*4 | kLdsSQ}.
+__device__ __forceinline__ uint32_t sq_map(const uint8_t *lds, uint32_t s, uint32_t jb) {
+  const uint32_t xl4 = ((s << 2) & 0x3C3C3C3Cu) | jb, xh4 = ((s >> 2) & 0x3C3C3C3Cu) | jb;
+  uint32_t t[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    t[2 * k] = lds_ld(lds, __builtin_amdgcn_perm(xl4, kLdsSQ, 0x0C020104u + k) + k * 512u);
+    t[2 * k + 1] = lds_ld(lds, __builtin_amdgcn_perm(xh4, kLdsSQ, 0x0C020104u + k) + k * 512u + 256u);
+  }
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+// Quarter row: lane L holds piece 4*(L&15) + (L>>4) of the row's last 1 KiB
+// (no transpose), i.e. 16-B piece hi = L>>4 of 64-B segment 48 + lo.  4 chain
+// steps, A_{16*(3-hi)} to the segment's end, XOR over lane bits 4 and 5, and
+// only row hi = 3 keeps it (m3: all-ones in lanes 48..63).
+__device__ __forceinline__ uint32_t quarter_row_segs(const uint8_t *lds, const u32x4 (&p)[4], uint32_t lsel,
+                                                     uint32_t jbq, uint32_t m3) {
+  uint32_t x = p[3][0];
+#pragma unroll
+  for (int d = 1; d < 4; ++d) x = slice4w(lds, x, p[3][d], lsel);
+  uint32_t a = sq_map(lds, slice4(lds, x, lsel), jbq);
+  a = xor_lanebit4(a);
+  a = xor_lanebit5(a);
+  return a & m3;
+}
+// Half row: the transpose's permlane16 stage on slots (2, 3) only leaves lane
+// L with the 32-B half (L >> 5) of 64-B segment 32 + (L & 31) in slots 2, 3.
+// 8 chain steps; the first halves (lower lanes) are shifted by A_32 and moved
+// to their upper partners by one permlane32_swap into a zero register:
+// upper lanes (mU all-ones) end with c ^ A_32(c_partner), lower lanes with 0.
+__device__ __forceinline__ uint32_t half_row_segs(const uint8_t *lds, u32x4 (&p)[4], uint32_t lsel, uint32_t mU) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    auto b = __builtin_amdgcn_permlane16_swap(p[2][d], p[3][d], false, false);
+    p[2][d] = b[0];
+    p[3][d] = b[1];
+  }
+  uint32_t x = p[2][0];
+#pragma unroll
+  for (int k = 2; k < 4; ++k)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (k == 2 && d == 0) continue;
+      x = slice4w(lds, x, p[k][d], lsel);
+    }
+  const uint32_t c = slice4(lds, x, lsel);
+  const uint32_t a = sq_map(lds, c, 0x40404040u); // j = 1: A_32
+  auto w = __builtin_amdgcn_permlane32_swap(0u, a, false, false); // w[0]: upper lanes <- a of lower lanes
+  return __builtin_amdgcn_bitop3_b32(c, mU, w[0], 0x6A);          // (c & mU) ^ w
 }
 
 struct QuarterInfo {
@@ -504,7 +571,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   static_assert(!STEAL || DYN, "stealing: DYN launches");
   constexpr uint32_t kRound = dyn_round(QB); // tasks per dealing round
   constexpr uint32_t kDynSlots = dyn_slots(QB);
-  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
+  // sub-row first rows: ragged QB = 1 with the plain chain (image V3 adds SQ)
+  constexpr bool kSub = kSubRows && QB == 1 && RAGGED && !kTwoChains &&
+                        (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblHalfChain)) == 0;
+  constexpr uint32_t kImgBytes = kSub ? kLdsBytesV3 : kLdsBytesV2;
+  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kImgBytes / 4];
   // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
   // rounds (generation), then the CRC ring (QB CRCs per task).
   __shared__ uint32_t s_ctl[DYN ? (STEAL ? dyn_ctl_words(QB) : dyn_ring_words(QB)) : 1];
@@ -527,7 +598,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   // All of this thread's image loads in flight at once (a rolled loop would
   // pay one L2 round trip per 16 KiB before the first HBM byte is read).
-  constexpr uint32_t kImgFull = kLdsBytesV2 / 16 / 1024, kImgRem = (kLdsBytesV2 / 16) % 1024;
+  constexpr uint32_t kImgFull = kImgBytes / 16 / 1024, kImgRem = (kImgBytes / 16) % 1024;
   // kEarly: the image in registers until the first row's loads are issued
   // (native vectors: HIP's uint4 struct copies became memcpys through a
   // private-memory array -- 160 B of scratch per lane).
@@ -537,7 +608,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   img_v img_t[kEarly ? kImgFull : 1];
   img_v img_r = img_v{0u, 0u, 0u, 0u};
   if constexpr (!kEarly) {
-    if constexpr ((ABL & kRowsAblNoImage) == 0) copy_lds_image<kLdsBytesV2>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
+    if constexpr ((ABL & kRowsAblNoImage) == 0) copy_lds_image<kImgBytes>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
     __syncthreads();
     if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();
   } else if constexpr ((ABL & kRowsAblNoImage) == 0) {
@@ -573,6 +644,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // byte offset of this lane's piece in a quarter
   const uint32_t pofs = 16u * (((ABL & kRowsAblNaturalOrder) != 0) ? lane : piece_of_lane(lane));
   const DistLane dl = dist_lane(lane);
+  // sub-row constants: quarter rows' SQ index j = hi, their kept row hi = 3;
+  // half rows' upper lanes
+  const uint32_t sub_jbq = (hi * 64u) * 0x01010101u;
+  const uint32_t sub_m3 = (hi == 3u) ? 0xFFFFFFFFu : 0u;
+  const uint32_t sub_mu = (lane & 32u) ? 0xFFFFFFFFu : 0u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // Task / item indices are 32-bit (launch_rows keeps every launch below 2^30
   // items): SALU has no 64-bit ordered compare, so 64-bit indices put every
@@ -958,7 +1034,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     auto compute = [&](bool valid, uint32_t hd, uint32_t len, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed,
                        uint32_t cidx, uint32_t tsk, u32x4 (&buf)[4]) {
       fix_row(hd, z, nr, r, buf);
-      const uint32_t v = quarter_crcs(buf);
+      uint32_t v;
+      if (kSub && r == 0 && hd <= kQuarter) v = merge_lo(lds, quarter_row_segs(lds, buf, lsel, sub_jbq, sub_m3), lsel1);
+      else if (kSub && r == 0 && hd <= 2 * kQuarter) v = merge_lo(lds, half_row_segs(lds, buf, lsel, sub_mu), lsel1);
+      else v = quarter_crcs(buf);
       RowMerge m;
       if constexpr ((ABL & kRowsAblNoMerge) == 0) {
         m = merge_row(lds, v, W, dl);
@@ -1078,9 +1157,20 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
              c_lp, c_len, c_z, c_seed);
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
         fix_row(c_lp, c_z, c_nr, c_r, cb);
-        transpose(cb);
-        const uint32_t ch = seg_crc(lds, cb, lsel);
-        const RowMerge pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
+        uint32_t ch;
+        RowMerge pm;
+        // (P's merge in each arm: the scheduler overlaps it with C's chain)
+        if (kSub && c_r == 0 && c_lp <= kQuarter) {
+          ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);
+          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
+        } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {
+          ch = half_row_segs(lds, cb, lsel, sub_mu);
+          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
+        } else {
+          transpose(cb);
+          ch = seg_crc(lds, cb, lsel);
+          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
+        }
         finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
         publish();
         p_ok = c_ok;

@@ -23,7 +23,7 @@ void nibble_table_inverse(uint32_t nbytes, uint32_t out[8][16]) {
 } // namespace
 
 void build_lds_image_v2(uint32_t *img) {
-  memset(img, 0, kLdsBytesV2);
+  memset(img, 0, kLdsBytesV3);
   uint8_t *b = reinterpret_cast<uint8_t *>(img);
   auto put = [&](uint32_t byte_addr, uint32_t v) { memcpy(b + byte_addr, &v, 4); };
   for (uint32_t v = 0; v < 256; ++v) {
@@ -57,6 +57,11 @@ void build_lds_image_v2(uint32_t *img) {
       for (uint32_t nib = 0; nib < 16; ++nib) put(kLdsZI2 + (z - 1) * 512 + n * 64 + nib * 4, nt[n][nib]);
   }
   for (uint32_t k = 0; k <= 256; ++k) put(kLdsTQ16 + 4 * k, gf2_shift_bytes(0xFFFFFFFFu, 16ull * k));
+  for (uint32_t j = 0; j < 4; ++j) { // sub-row shifts A_{16*(3-j)} (crc32_layout.h SQ)
+    nibble_table(16u * (3u - j), nt);
+    for (uint32_t n = 0; n < 8; ++n)
+      for (uint32_t nib = 0; nib < 16; ++nib) put(sq_byte(j, n, nib), nt[n][nib]);
+  }
 }
 
 void build_scalar_tab(uint32_t *tab) {

@@ -385,13 +385,13 @@ void init_device(int dev) {
   c.cus = prop.multiProcessorCount;
   snprintf(c.name, sizeof c.name, "%s", prop.name);
   snprintf(c.arch, sizeof c.arch, "%s", prop.gcnArchName);
-  if (prop.sharedMemPerBlock < kLdsBytesV2) { // needs the 160 KiB LDS of gfx950
+  if (prop.sharedMemPerBlock < kLdsBytesV3) { // needs the 160 KiB LDS of gfx950
     fprintf(stderr, "rpccrc: device %d (%s) has %zu B LDS per block, need %u\n", dev, c.arch,
-            (size_t)prop.sharedMemPerBlock, kLdsBytesV2);
+            (size_t)prop.sharedMemPerBlock, kLdsBytesV3);
     c.status = RPCCRC_ENODEV;
     return;
   }
-  std::vector<uint32_t> img(kLdsBytesV2 / 4), tq(kTqEntries), nib(kShiftNibWords), stab(kScalarTabWords);
+  std::vector<uint32_t> img(kLdsBytesV3 / 4), tq(kTqEntries), nib(kShiftNibWords), stab(kScalarTabWords);
   build_tq(tq.data());
   build_scalar_tab(stab.data());
   uint32_t sq = kX0 >> 8; // x^8 (one zero byte); squared: x^(8 * 2^k)
@@ -404,7 +404,7 @@ void init_device(int dev) {
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);
   hipError_t e = hipSuccess;
-  e = (e == hipSuccess) ? hipMalloc(&c.img, kLdsBytesV2) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.img, kLdsBytesV3) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.scalar_tab, kScalarTabWords * 4) : e;
@@ -412,7 +412,7 @@ void init_device(int dev) {
   if (e == hipSuccess) *reinterpret_cast<volatile uint32_t *>(c.err) = 0;
   if (e == hipSuccess) {
     build_lds_image_v2(img.data());
-    e = hipMemcpy(c.img, img.data(), kLdsBytesV2, hipMemcpyHostToDevice);
+    e = hipMemcpy(c.img, img.data(), kLdsBytesV3, hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);

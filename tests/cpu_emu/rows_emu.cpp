@@ -7,7 +7,8 @@
 // with the oracle by tests/test_kernel_emu.py.  Not the product path.
 //
 // stdin:  QB misalign n  then n lengths; bodies are splitmix bytes (seed 7)
-//         back to back from byte `misalign` of a 16-aligned buffer.
+//         back to back from byte `misalign` of a 16-aligned buffer.  QB = 1 is
+//         the ragged kernel (sub-row first rows), QB = 5 QB = 1 with full rows.
 //         QB = 2 is the packed ragged kernel (crc32_packed.h) and reads
 //         "nwaves min_slice max_slices" after n.
 // stdout: one CRC (hex) per body.
@@ -25,7 +26,7 @@ using namespace rpccrc;
 
 static std::vector<uint32_t> g_img, g_tq;
 static uint32_t ld(uint32_t a) {
-  if (a % 4 || a >= kLdsBytesV2) { fprintf(stderr, "bad lds addr %u\n", a); exit(2); }
+  if (a % 4 || a >= kLdsBytesV3) { fprintf(stderr, "bad lds addr %u\n", a); exit(2); }
   return g_img[a / 4];
 }
 static uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
@@ -182,6 +183,64 @@ static void merge_lo(Wave s) {
   row_ror(s, t, 8); for (int l = 0; l < 64; ++l) s[l] ^= t[l];
 }
 
+// Sub-row first rows (ragged QB = 1, crc32_rows.h sub_chain): per-lane SQ
+// shift A_{16*(3-j)} with the perm-formed address {j*64 + nib*4 | kLdsSQ},
+// nibble n's 256-B block in the immediate.
+static uint32_t sq_map(uint32_t s, uint32_t j) {
+  const uint32_t jb = (j * 64u) * 0x01010101u;
+  const uint32_t xl4 = ((s << 2) & 0x3C3C3C3Cu) | jb, xh4 = ((s >> 2) & 0x3C3C3C3Cu) | jb;
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    r ^= ld(perm(xl4, kLdsSQ, 0x0C020104u + k) + k * 512u);
+    r ^= ld(perm(xh4, kLdsSQ, 0x0C020104u + k) + k * 512u + 256u);
+  }
+  return r;
+}
+static uint32_t chain_slots(const Piece *slots, int nslots, uint32_t lane) {
+  const uint32_t lane4 = (lane & 31u) * 4u, lsel = lane4 | ((lane4 + 128u) << 8) | (1u << 16);
+  uint32_t x = slots[0].d[0];
+  for (int k = 0; k < nslots; ++k)
+    for (int d = 0; d < 4; ++d) {
+      if (!k && !d) continue;
+      x = slice4(x, lsel) ^ slots[k].d[d];
+    }
+  return slice4(x, lsel);
+}
+// Quarter row (hd <= 1 KiB: only load 3 holds data): no transpose, 4 chain
+// steps on slot 3, A_{16*(3-hi)}, XOR over lane bits 4 and 5, rows hi < 3 zeroed.
+// Half row (hd <= 2 KiB: loads 2, 3): the transpose's permlane16 stage on
+// slots (2, 3) only -- lane L then holds the 32-B half (L >> 5) of 64-B
+// segment 32 + (L & 31); 8 chain steps; lower lanes' A_32 moved up by one
+// permlane32_swap into a zero register and XORed into the upper lanes.
+// Both leave the full-row layout (lane L' = 64-B segment L') for merge_lo.
+static void sub_chain(Piece P[4][64], bool quarter, Wave v) {
+  if (quarter) {
+    Wave a;
+    for (int l = 0; l < 64; ++l) a[l] = sq_map(chain_slots(&P[3][l], 1, (uint32_t)l), (uint32_t)l >> 4);
+    xor_lanebit(a, 4);
+    xor_lanebit(a, 5);
+    for (int l = 0; l < 64; ++l) v[l] = ((l >> 4) == 3) ? a[l] : 0u;
+    return;
+  }
+  for (int d = 0; d < 4; ++d) {
+    Wave w2, w3;
+    for (int l = 0; l < 64; ++l) { w2[l] = P[2][l].d[d]; w3[l] = P[3][l].d[d]; }
+    permlane16_swap(w2, w3);
+    for (int l = 0; l < 64; ++l) { P[2][l].d[d] = w2[l]; P[3][l].d[d] = w3[l]; }
+  }
+  Wave c, a, zr;
+  for (int l = 0; l < 64; ++l) {
+    Piece sl[2] = {P[2][l], P[3][l]};
+    c[l] = chain_slots(sl, 2, (uint32_t)l);
+    a[l] = sq_map(c[l], 1u);
+    zr[l] = 0u;
+  }
+  permlane32_swap(zr, a);
+  for (int l = 0; l < 64; ++l) v[l] = ((l & 32) ? c[l] : 0u) ^ zr[l];
+}
+
+static bool g_subrows = true; // QB code 1: sub-row first rows (the ragged kernel); 5: full rows only
+
 static void mask_piece(Piece &p, int64_t v, int64_t len) {
   for (int d = 0; d < 4; ++d) {
     int64_t lo = v + 4 * d;
@@ -217,7 +276,9 @@ static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
         if (rs < 0 || (last && z)) mask_piece(P[b][L], v, len);
       }
     Wave s;
-    row_chain(P, s);
+    const uint32_t hd = r == 0 ? first : 4096u;
+    if (g_subrows && !kTwoChains && hd <= 2048u) sub_chain(P, hd <= 1024u, s);
+    else row_chain(P, s);
     merge_lo(s);
     for (int h = 0; h < 4; ++h)
       for (int l = 16 * h; l < 16 * h + 16; ++l)
@@ -523,7 +584,7 @@ int main() {
     if (scanf("%u", &lens[i]) != 1) return 1;
     total += lens[i];
   }
-  g_img.resize(kLdsBytesV2 / 4);
+  g_img.resize(kLdsBytesV3 / 4);
   build_lds_image_v2(g_img.data());
   g_tq.resize(kTqEntries);
   build_tq(g_tq.data());
@@ -545,6 +606,10 @@ int main() {
   for (unsigned long i = 0; i < n; ++i) {
     ptr[i] = buf + off;
     off += lens[i];
+  }
+  if (QB == 5) { // QB = 1 with full rows only
+    QB = 1;
+    g_subrows = false;
   }
   if (QB == 1) {
     for (unsigned long i = 0; i < n; ++i) printf("%08x\n", emu_qb1(ptr[i], lens[i]));

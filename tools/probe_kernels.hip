@@ -16,12 +16,12 @@ uint32_t *g_tq = nullptr;
 
 int ensure_tables() {
   if (g_img) return 0;
-  std::vector<uint32_t> img(kLdsBytesV2 / 4), tq(kTqEntries);
+  std::vector<uint32_t> img(kLdsBytesV3 / 4), tq(kTqEntries);
   build_lds_image_v2(img.data());
   build_tq(tq.data());
-  if (hipMalloc(&g_img, kLdsBytesV2) != hipSuccess) return -1;
+  if (hipMalloc(&g_img, kLdsBytesV3) != hipSuccess) return -1;
   if (hipMalloc(&g_tq, kTqEntries * 4) != hipSuccess) return -1;
-  if (hipMemcpy(g_img, img.data(), kLdsBytesV2, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (hipMemcpy(g_img, img.data(), kLdsBytesV3, hipMemcpyHostToDevice) != hipSuccess) return -1;
   if (hipMemcpy(g_tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
   return 0;
 }
