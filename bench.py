@@ -364,8 +364,14 @@ def frames_lifted_probe(device, n=1024, reps=5, seed=0x5EED0007):
     stream = torch.cuda.current_stream()
 
     def timed(fn):
-        fn()
-        torch.cuda.synchronize()
+        # clock prewarm as for the main line (the first ~20 launches of sustained
+        # load run 15-30 % slower while the clock settles)
+        t0 = time.perf_counter()
+        while True:
+            fn()
+            torch.cuda.synchronize()
+            if time.perf_counter() - t0 >= 0.3:
+                break
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(reps):

@@ -346,6 +346,7 @@ constexpr int kRowsAblNtStore = 2048; // non-temporal CRC stores (DYN paths; exa
 // Chain only slots 2-3 (8 slice-by-4 steps per lane, the last 2 KiB of the row):
 // the instruction cost of a half-width row (timing only: wrong CRCs).
 constexpr int kRowsAblHalfChain = 8192;
+constexpr int kRowsAblNoSub = 16384; // ragged QB = 1 without the quarter / half first rows (exact)
 // QB = 1 software pipeline over rows (chain of row r+1 beside the merge of row r).
 #ifndef RPCCRC_ROWS_PIPE
 #define RPCCRC_ROWS_PIPE 1
@@ -573,7 +574,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   constexpr uint32_t kDynSlots = dyn_slots(QB);
   // sub-row first rows: ragged QB = 1 with the plain chain (image V3 adds SQ)
   constexpr bool kSub = kSubRows && QB == 1 && RAGGED && !kTwoChains &&
-                        (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblHalfChain)) == 0;
+                        (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblHalfChain | kRowsAblNoSub)) == 0;
   constexpr uint32_t kImgBytes = kSub ? kLdsBytesV3 : kLdsBytesV2;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kImgBytes / 4];
   // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot

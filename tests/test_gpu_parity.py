@@ -250,9 +250,10 @@ def test_device_batch_tiny_bodies(misalign, ragged_path):
 
 
 def test_device_batch_chunk_boundaries(ragged_path):
-    """Lengths around the 1 KiB chunk and 4 KiB row boundaries, at every misalignment."""
-    base_lens = [1008, 1009, 1016, 1023, 1024, 1025, 1040, 2047, 2048, 2049, 3071, 3072, 3073, 4095, 4096,
-                 4097, 5119, 5120, 8191, 8192, 8193]
+    """Lengths around the 1 KiB chunk and 4 KiB row boundaries, at every misalignment
+    (and the rows kernel's quarter / half first rows: first-row bytes incl. pad <= 1024 / 2048)."""
+    base_lens = [1008, 1009, 1016, 1023, 1024, 1025, 1040, 2032, 2033, 2047, 2048, 2049, 2064, 3071, 3072, 3073,
+                 4095, 4096, 4097, 5104, 5105, 5119, 5120, 6128, 6129, 6143, 6144, 6145, 8191, 8192, 8193]
     lens = np.array([L for L in base_lens for _ in range(16)] * 3, dtype=np.uint32)
     offs = np.empty(len(lens), dtype=np.uint64)
     pos = 0

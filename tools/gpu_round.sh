@@ -60,6 +60,7 @@ for s in $STEPS; do
                    --only qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl9216_d1,qb1_pair1_nt1_abl1027_d1 ;;
     prof_frames) run prof_frames 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_frames" -o run --output-format csv -- \
                    python3 tools/frames_lifted.py 3 ;;
+    ragged) run ragged_${RAGGED_CFG:-c2} 300 python tools/probe.py --mode ragged --config ${RAGGED_CFG:-c2} --rounds ${RAGGED_ROUNDS:-3} --reps 5 ;;
     bench_scalar) run bench_scalar 300 tools/scalar_bench oracle/_ref/libref_crc.so ;;
     bench) run bench 600 python bench.py ;;
     probe) run probe 600 python tools/probe.py ;;

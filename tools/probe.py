@@ -227,6 +227,54 @@ def packed_modes(a):
         torch.cuda.empty_cache()
 
 
+def ragged_ablate(a):
+    """Ragged QB = 1 rows kernel (DYN, the C2 path) under ablation bits on a
+    ragged workload (--config c2): what bounds it -- memory, compute, stores,
+    the quarter / half first rows.  Interleaved rounds, median; exact variants
+    (0, 16384) are checked against the product's CRCs."""
+    import time
+    so = os.path.join(REPO, "tools", "libprobe.so")
+    lib = ctypes.CDLL(so)
+    lib.probe_rows_ragged.restype = ctypes.c_int
+    lib.probe_rows_ragged.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    w = Workload(a.config, 0, torch.device("cuda", 0))
+    assert w.kind == "ragged", "ragged mode needs a ragged config (c2)"
+    out = torch.empty(w.n, dtype=torch.int32, device=w.device)
+    s = torch.cuda.current_stream()
+    names = {0: "product", 16384: "full first rows (no sub-rows)", 3: "memory only", 4: "compute only",
+             16: "no stores", 2: "no merge", 19: "memory only, no stores"}
+    if a.only:
+        names = {k: v for k, v in names.items() if str(k) in a.only.split(",")}
+
+    def mk(abl):
+        def f():
+            rc = lib.probe_rows_ragged(w.base.data_ptr(), w.offs.data_ptr(), w.lens.data_ptr(), w.n, out.data_ptr(),
+                                       abl, 256, s.cuda_stream)
+            assert rc == 0, (abl, rc)
+        return f
+    w.step()
+    torch.cuda.synchronize()
+    ref = w.out.clone()
+    for abl in (0, 16384):
+        if abl in names:
+            mk(abl)()
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), f"ragged variant {abl} changed the CRCs"
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        mk(0)()
+    torch.cuda.synchronize()
+    res = {k: [] for k in names}
+    for _ in range(a.rounds):
+        for k in names:
+            res[k].append(timed(mk(k), a.reps))
+    for k, ts in res.items():
+        med = statistics.median(ts)
+        print(json.dumps({"mode": "ragged", "config": a.config, "abl": k, "variant": names[k],
+                          "median_us": round(med * 1e6, 1), "frac": round(w.algo_bytes / med / 8e12, 4)}), flush=True)
+
+
 def stream_rows(a):
     """Row-shape stream probes (tools/probe_kernels.hip stream_rows_probe): per
     mode, GB/s and tiles (wave iterations) per us over the north-star buffer,
@@ -348,7 +396,7 @@ def main():
     ap.add_argument("--grids", default="0,512,1024")
     ap.add_argument("--shapes", default="", help="packed mode: comma list of shapes (default all)")
     ap.add_argument("--paths", default="rows,packed", help="packed mode: ragged paths to time")
-    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline", "packed", "streamrows"])
+    ap.add_argument("--mode", default="lib", choices=["lib", "ablate", "sustain", "timeline", "packed", "streamrows", "ragged"])
     ap.add_argument("--launches", type=int, default=60)
     ap.add_argument("--smi-out", default="", help="sustain mode: raw SMI samples (jsonl)")
     ap.add_argument("--only", default="", help="comma list of ablate variant names")
@@ -362,6 +410,8 @@ def main():
         return packed_modes(a)
     if a.mode == "streamrows":
         return stream_rows(a)
+    if a.mode == "ragged":
+        return ragged_ablate(a)
     w = Workload(a.config, 0, torch.device("cuda", 0))
     if a.mode == "sustain":
         return sustain(w, a)

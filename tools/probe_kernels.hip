@@ -98,6 +98,44 @@ extern "C" __attribute__((visibility("default"))) int probe_rows(const uint8_t *
                           pair >> 8);
 }
 
+// Ragged QB = 1 DYN rows kernel (the C2 path, static rounds) under ablation
+// bits: 0 product, kRowsAblNoSub full first rows, 3 memory only, 4 compute
+// only (synthesized rows, metadata still read), 16 no stores, 2 no merge.
+template <int ABL>
+void go_ragged(const ItemsArgs &a, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL((crc32_rows_kernel<1, true, true, ABL, 1, true>), dim3(blocks), dim3(1024), 0, s, a);
+}
+extern "C" __attribute__((visibility("default"))) int probe_rows_ragged(const uint8_t *d_base, const uint64_t *d_offs,
+                                                                         const uint32_t *d_lens, uint64_t n,
+                                                                         uint32_t *d_out, int abl, int blocks,
+                                                                         void *stream) {
+  if (ensure_tables()) return -12;
+  ItemsArgs a;
+  a.base = d_base;
+  a.offsets = d_offs;
+  a.lengths = d_lens;
+  a.n_items = n;
+  a.stride = 0;
+  a.len = 0;
+  a.mode = kModeFinal;
+  a.lds_image = g_img;
+  a.tq = g_tq;
+  a.out = d_out;
+  a.gshift = 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (abl) {
+  case 0: go_ragged<0>(a, blocks, s); break;
+  case kRowsAblNoSub: go_ragged<kRowsAblNoSub>(a, blocks, s); break;
+  case 3: go_ragged<3>(a, blocks, s); break;
+  case 4: go_ragged<4>(a, blocks, s); break;
+  case 16: go_ragged<16>(a, blocks, s); break;
+  case 2: go_ragged<2>(a, blocks, s); break;
+  case 3 | 16: go_ragged<3 | 16>(a, blocks, s); break;
+  default: return -22;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 // ---------------------------------------------------------------------------
 // Row-shape stream probes (MEASUREMENT ONLY): does a wave-iteration cost track
 // the bytes it reads or the load instructions it issues?  Tile t of TB bytes
