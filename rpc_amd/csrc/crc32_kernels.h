@@ -82,6 +82,11 @@ struct BigRoute {
   uint32_t *c_len;
   uint32_t *c_raw;
   uint64_t min_chunk = kBigMinChunk; // the plan's starting chunk size (power of two)
+  // Route-all mode (all_n > 0): every body of a batch of all_n <= kBigMaxBodies
+  // takes the route, body b = batch index b (no classify pass, no b_idx list,
+  // no plain rows pass); the plan sums the lengths itself.
+  uint32_t all_n = 0;
+  const uint32_t *tq = nullptr; // Tq[q] = A_q(0xFFFFFFFF): the combine seeds chunk 0 with it
 };
 size_t big_route_workspace_bytes(uint64_t n);
 BigRoute big_route_carve(void *ws, uint64_t n);
@@ -90,8 +95,8 @@ BigRoute big_route_carve(void *ws, uint64_t n);
 // big_min: bodies of at least this many bytes are routed (kBigMin by default).
 hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big_min, const BigRoute &r,
                                hipStream_t s);
-// After the rows pass: chunk plan, chunk CRCs (rows kernel, RAW), per-body
-// fold into out[batch index].
+// After the rows pass (route-all: instead of it): chunk plan, chunk CRCs (rows
+// kernel, RAW), per-body fold into out[batch index].
 // steal: a leased zeroed two-word counter for the chunk pass's tail stealing
 // (nullptr: static rounds); its event is recorded as the chunk pass's
 // completion (steal_done, *steal_recorded) like launch_rows.

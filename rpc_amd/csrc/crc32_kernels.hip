@@ -576,11 +576,14 @@ __global__ void __launch_bounds__(256) big_classify_kernel(const uint32_t *lengt
 }
 
 __device__ __forceinline__ uint64_t big_count(const BigRoute &r) {
+  if (r.all_n) return r.all_n;
   const uint64_t c = r.meta[0];
   return c < kBigMaxBodies ? c : kBigMaxBodies;
 }
+__device__ __forceinline__ uint32_t big_body(const BigRoute &r, uint64_t b) { return r.all_n ? (uint32_t)b : r.b_idx[b]; }
 
-// One block: chunk size, per-body chunk counts and their exclusive scan.
+// One block: chunk size, per-body chunk counts and their exclusive scan
+// (route-all: also the routed bytes, which classify sums otherwise).
 __global__ void __launch_bounds__(1024) big_plan_kernel(const uint32_t *lengths, BigRoute r) {
   __shared__ unsigned long long wsum[16];
   __shared__ unsigned long long run;
@@ -593,16 +596,29 @@ __global__ void __launch_bounds__(1024) big_plan_kernel(const uint32_t *lengths,
     }
     return;
   }
+  uint64_t bytes;
+  if (r.all_n) {
+    unsigned long long x = 0;
+    for (uint64_t b = t; b < nb; b += 1024) x += lengths[b];
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    if (lane == 0) wsum[w] = x;
+    __syncthreads();
+    bytes = 0;
+    for (uint32_t k = 0; k < 16; ++k) bytes += wsum[k];
+    __syncthreads();
+  } else {
+    bytes = r.meta[1];
+  }
   // Chunks of (2^k) * 4096 - 16 bytes: end-aligned chunks all share their body's
   // end pad z < 16, so each takes exactly 2^k rows (a 4096-byte chunk with
   // z != 0 would take two).  sum ceil(len / chunk) <= bytes / chunk + 1 + nb
   uint64_t chunk = r.min_chunk;
-  while (r.meta[1] / chunk + 1 + nb > kBigMaxChunks) chunk = ((chunk + 16) << 1) - 16;
+  while (bytes / chunk + 1 + nb > kBigMaxChunks) chunk = ((chunk + 16) << 1) - 16;
   if (t == 0) run = 0;
   __syncthreads();
   for (uint64_t base = 0; base < nb; base += 1024) {
     const uint64_t b = base + t;
-    const unsigned long long c = (b < nb) ? ((uint64_t)lengths[r.b_idx[b]] + chunk - 1) / chunk : 0ull;
+    const unsigned long long c = (b < nb) ? ((uint64_t)lengths[big_body(r, b)] + chunk - 1) / chunk : 0ull;
     unsigned long long x = c; // inclusive wave scan
     for (int d = 1; d < 64; d <<= 1) {
       const unsigned long long y = __shfl_up(x, d, 64);
@@ -625,39 +641,44 @@ __global__ void __launch_bounds__(1024) big_plan_kernel(const uint32_t *lengths,
 }
 
 // Chunk table: end-aligned chunks of each routed body (the first one partial).
+// Block k takes bodies k, k + grid, ...; its threads stride over the body's
+// chunks (round 2 searched the body of every chunk: ~9 dependent global loads
+// per chunk, 20 us for 0.9M chunks).
 __global__ void __launch_bounds__(256) big_expand_kernel(const uint64_t *offsets, const uint32_t *lengths, BigRoute r) {
-  const uint64_t total = r.meta[2], nb = big_count(r), chunk = r.meta[3];
-  for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256u) {
-    uint64_t lo = 0, hi = nb; // last body with b_first <= t (every body has >= 1 chunk)
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) / 2;
-      if (r.b_first[mid] <= t) lo = mid; else hi = mid;
+  const uint64_t nb = big_count(r), chunk = r.meta[3];
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t i = big_body(r, b);
+    const uint64_t L = lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first, off = offsets[i];
+    for (uint64_t k = threadIdx.x; k < nch; k += 256) {
+      const uint64_t end = L - (nch - 1 - k) * chunk;
+      const uint64_t start = end > chunk ? end - chunk : 0;
+      r.c_off[first + k] = off + start;
+      r.c_len[first + k] = (uint32_t)(end - start);
     }
-    const uint32_t i = r.b_idx[lo];
-    const uint64_t L = lengths[i], nch = r.b_first[lo + 1] - r.b_first[lo], k = t - r.b_first[lo];
-    const uint64_t end = L - (nch - 1 - k) * chunk;
-    const uint64_t start = end > chunk ? end - chunk : 0;
-    r.c_off[t] = offsets[i] + start;
-    r.c_len[t] = (uint32_t)(end - start);
   }
 }
 
 // Persistent fold: block b takes routed bodies b, b + grid, ...: thread t runs
-// Horner over chunks t, t + 1024, ... with the step map A_{1024 * chunk} (built
-// once per block as one nibble table: the chunk is 2^k * 4096 - 16 bytes, not a
-// power of two), shifts its partial to the body end, and the block
-// XOR-reduces: crc = ~(A_L(F) ^ XOR_k A_{(nch-1-k) chunk}(raw_k)).
+// Horner over chunks t, t + 1024, ... with the step map A_{1024 * chunk},
+// shifts its partial by A_{j * chunk} to the body end (j = chunks after its
+// last one, < 1024: one map per set bit of j from the doubling tables
+// A_{chunk * 2^i}), and the block XOR-reduces:
+//   crc = ~(XOR_k A_{(nch-1-k) chunk}(raw_k)),  raw_0 ^= A_{len_0}(F):
+// the zlib pre-conditioning enters with chunk 0 (Tq for len_0 <= 4096), so no
+// shift by the whole body length follows the reduction.  (The chunk is
+// 2^k * 4096 - 16 bytes, not a power of two: the maps are built per block.)
 __device__ __forceinline__ uint32_t nib_map(const uint32_t *m, uint32_t v) {
   uint32_t r = 0;
 #pragma unroll
   for (uint32_t i = 0; i < 8; ++i) r ^= m[i * 16u + ((v >> (4u * i)) & 15u)];
   return r;
 }
+constexpr uint32_t kBigDbl = 11; // A_{chunk * 2^i}, i = 0..10 (i = 10: the Horner step)
 __global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengths, BigRoute r, const uint4 *shift_nib,
                                                            uint32_t *out) {
   __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
   __shared__ uint32_t part[16];
-  __shared__ uint32_t stepnib[128]; // [i][j] = A_{1024 * chunk}(j << 4i)
+  __shared__ uint32_t dbl[kBigDbl * 128]; // [i][n][j] = A_{chunk * 2^i}(j << 4n)
   const uint64_t nb = big_count(r);
   if (blockIdx.x >= nb) return;
   const uint32_t t = threadIdx.x;
@@ -667,24 +688,38 @@ __global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengt
     for (uint32_t q = 0; q < kShiftNibWords / 4 / 1024; ++q) dst[q * 1024 + t] = shift_nib[q * 1024 + t];
   }
   __syncthreads();
-  const uint64_t chunk = r.meta[3], step = 1024ull * chunk;
-  if (t < 128) stepnib[t] = nib_shift(nib, step, (t & 15u) << (4u * (t >> 4)));
+  const uint64_t chunk = r.meta[3];
+  for (uint32_t e = t; e < kBigDbl * 128; e += 1024) {
+    const uint32_t i = e >> 7, x = e & 127u;
+    dbl[e] = nib_shift(nib, chunk << i, (x & 15u) << (4u * (x >> 4)));
+  }
   __syncthreads();
+  const uint32_t *stepnib = dbl + 10 * 128; // A_{1024 * chunk}
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    const uint32_t i = r.b_idx[b];
+    const uint32_t i = big_body(r, b);
     const uint64_t L = lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first;
     uint32_t acc = 0;
-    for (uint64_t k = t; k < nch; k += 1024) acc = nib_map(stepnib, acc) ^ r.c_raw[first + k];
+    for (uint64_t k = t; k < nch; k += 1024) {
+      uint32_t raw = r.c_raw[first + k];
+      if (k == 0) { // zlib's pre-conditioning, carried from the body's first byte
+        const uint64_t len0 = L - (nch - 1) * chunk;
+        raw ^= (len0 < kTqEntries) ? r.tq[len0] : nib_shift(nib, len0, 0xFFFFFFFFu);
+      }
+      acc = nib_map(stepnib, acc) ^ raw;
+    }
     if (t < nch) {
-      const uint64_t kl = t + (nch - 1 - t) / 1024 * 1024;
-      acc = nib_shift(nib, (nch - 1 - kl) * chunk, acc);
+      uint32_t j = (uint32_t)((nch - 1 - t) % 1024u); // chunks after this thread's last one
+      while (j) {
+        acc = nib_map(dbl + 128u * (uint32_t)__builtin_ctz(j), acc);
+        j &= j - 1;
+      }
     }
     for (int m = 1; m < 64; m <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, m, 64);
     if ((t & 63u) == 0) part[t >> 6] = acc;
     __syncthreads();
     if (t == 0) {
       for (uint32_t w = 1; w < 16; ++w) acc ^= part[w];
-      out[i] = acc ^ ~nib_shift(nib, L, 0xFFFFFFFFu);
+      out[i] = nch ? ~acc : 0u; // an empty body: crc32 = 0
     }
     __syncthreads();
   }

@@ -361,6 +361,7 @@ const uint32_t g_big_chunk = [] {
 }();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kSplitMinFrames = 16384;       // fewer frames: one wave per body (rows kernel)
+constexpr uint64_t kRouteAllMax = 2048;           // lifted-cap frames batches up to this size: route-all
 constexpr bool kAutoSplitFrames = true;           // AUTO frames batches: split (true) or packed (false)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
 // Chunks per packed slice, at least: a slice switch costs the wave two scalar
@@ -588,13 +589,25 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     if (const int rc = ws.get(c.ws, split_bytes + route_bytes, s)) return rc;
   BigRoute r{};
   StealLease sl; // the route's chunk pass deals its tail from this counter (device-counted)
+  // Route-all: a lifted-cap frames batch of at most kRouteAllMax frames sends
+  // every body through the chunk route (no classify pass and no plain rows
+  // pass, whose longest non-routed body -- up to the 16 KiB small-batch
+  // threshold, one wave -- set its duration: 15 us of a 1024-frame verify).
+  // Bounded because the fold spends a block-wide reduction per body (256
+  // blocks): a few bodies per block cost less than the passes they replace.
+  const bool route_all = route && small_bodies && !split && n <= kRouteAllMax && !g_big_min_env;
   if (route) {
-    const uint32_t big_min = big_min_for(n);
     r = big_route_carve(ws.ptr() + split_bytes, n);
     r.min_chunk = g_big_chunk;
-    RPCCRC_TRY(launch_big_classify(lengths, n, big_min, r, s));
-    a.routed = r.routed;
-    a.big_min = big_min;
+    r.tq = c.tq;
+    if (route_all) {
+      r.all_n = (uint32_t)n;
+    } else {
+      const uint32_t big_min = big_min_for(n);
+      RPCCRC_TRY(launch_big_classify(lengths, n, big_min, r, s));
+      a.routed = r.routed;
+      a.big_min = big_min;
+    }
     if (const int rc = c.steal->acquire(s, &sl.slot)) return rc;
     sl.p = sl.slot->p;
     sl.pool = c.steal;
@@ -602,7 +615,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   }
   if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
-  } else {
+  } else if (!route_all) {
     RPCCRC_TRY(launch_rows(a, 1, nt, mb, s));
   }
   if (route) RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s, sl.p, sl.done_event(), &sl.recorded));

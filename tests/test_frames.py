@@ -229,6 +229,27 @@ def test_frames_lifted_cap_large_bodies(frames_path):
     assert v[9] == v[12] == rpc_amd.FRAME_BAD_CRC
 
 
+@pytest.mark.parametrize("role", ["server", "client"])
+def test_frames_lifted_cap_route_all_mixed(role):
+    """A small lifted-cap batch (route-all: every body through the chunk route, no
+    classify or plain rows pass) with every verdict the parse decides: heartbeats of
+    both types, empty bodies, a bad CRC, bodies around the 4080-byte chunk and the
+    4096-entry Tq seed table, a header whose body runs past the stream."""
+    rng = np.random.default_rng(23 if role == "server" else 24)
+    frames = []
+    for L in [0, 1, 15, 16, 1024, 1025, 4079, 4080, 4081, 4096, 4097, 8160, 8161, 20000, 300000, 0, 77]:
+        b = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        frames.append(header(L, oracle.crc32(np.frombuffer(b, dtype=np.uint8)) if L else 0) + b)
+    frames.append(header(0, 0, type_=rpc_amd.RPC_TYPE_PING))
+    frames.append(header(5, 123, type_=rpc_amd.RPC_TYPE_PONG) + b"abcde")
+    b = rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()
+    frames.append(header(5000, oracle.crc32(np.frombuffer(b, dtype=np.uint8)) ^ 1) + b)  # bad CRC
+    frames.append(header(1 << 20, 7) + b"short")  # runs past the stream
+    blob, offs = layout(frames, gap=3)
+    got = verify(blob, offs, role=role, lift_cap=True)
+    assert got == expected(blob, offs, role=role, lift_cap=True)
+
+
 def test_frames_role_flags_rejected():
     d = to_dev(np.zeros(64, dtype=np.uint8))
     o = to_dev(np.zeros(1, dtype=np.int64))

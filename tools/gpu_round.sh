@@ -58,6 +58,10 @@ for s in $STEPS; do
     ab) run ab 1200 bash tools/ab_lib.sh "$TAG/ab" "${AB_LIBS:-head}" "${AB_CFGS:-ns}" "${AB_ROUNDS:-2}" ;;
     ablate_half) run ablate_half 600 python tools/probe.py --mode ablate --rounds 3 --config u2k \
                    --only qb1_pair1_nt1_abl1024_d1,qb1_pair1_nt1_abl9216_d1,qb1_pair1_nt1_abl1027_d1 ;;
+    frames_chunks)
+           for k in ${FRAMES_CHUNKS:-4080 8176 16368}; do
+             RPCCRC_BIG_CHUNK=$k run frames_chunk$k 300 python tools/frames_lifted.py 3 || exit 1
+           done ;;
     prof_frames) run prof_frames 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_frames" -o run --output-format csv -- \
                    python3 tools/frames_lifted.py 3 ;;
     ragged) run ragged_${RAGGED_CFG:-c2} 300 python tools/probe.py --mode ragged --config ${RAGGED_CFG:-c2} --rounds ${RAGGED_ROUNDS:-3} --reps 5 ;;
