@@ -68,11 +68,13 @@ constexpr uint32_t kErrRingWait = 2u;  // a wave gave up waiting for an output-r
 constexpr uint32_t kBigMin = 256u << 10;
 constexpr uint32_t kBigMaxBodies = 16384;
 constexpr uint64_t kBigMaxChunks = 1ull << 20;
-// Default first chunk size: one-row chunks (4080 B: with the body's end pad
-// z <= 15 a chunk still fits one 4 KiB row), so the chunk pass deals its tail
-// with stealing (16 KiB chunks until round 3, five rows each when z != 0).
+// Default first chunk size: two-row chunks (8176 B: with the body's end pad
+// z <= 15 a chunk still fits two 4 KiB rows), dealt with tail stealing.
+// 1024 lifted-cap frames of 1 B - 64 MiB (bench extra.frames_lifted), verify
+// per call on one box: 4080 B 622-634 us, 8176 B 590-596 us, 16368 B 602-609 us
+// (profiles/r03d/frames_chunks.txt); 16 KiB chunks until round 3.
 // The plan grows it as (chunk + 16) * 2 - 16 until the chunks fit kBigMaxChunks.
-constexpr uint64_t kBigMinChunk = 4096 - 16;
+constexpr uint64_t kBigMinChunk = 8192 - 16;
 struct BigRoute {
   uint32_t *routed;  // bit i: body i takes the route (ceil(n / 64) * 2 words, all written)
   uint64_t *meta;    // [0] bodies claimed, [1] their bytes, [2] chunks, [3] chunk bytes
@@ -86,8 +88,17 @@ struct BigRoute {
   // takes the route, body b = batch index b (no classify pass, no b_idx list,
   // no plain rows pass); the plan sums the lengths itself.
   uint32_t all_n = 0;
-  const uint32_t *tq = nullptr; // Tq[q] = A_q(0xFFFFFFFF): the combine seeds chunk 0 with it
+  const uint32_t *tq = nullptr;  // Tq[q] = A_q(0xFFFFFFFF): the combine seeds chunk 0 with it
+  const uint32_t *dbl = nullptr; // kBigDblWords: the fold's doubling maps per chunk class (build_big_dbl)
 };
+// The fold's maps, built once per device on the host: for chunk class m
+// (chunk = 4096 * 2^m - 16 bytes, m < kBigChunkClasses) and i < kBigDbl,
+// DBL[m][i][n][j] = A_{chunk * 2^i}(j << 4n).  (Round 3 built them in every
+// fold block from the 32 KiB A_{2^k} maps: ~10 us of a 24 us fold.)
+constexpr uint32_t kBigChunkClasses = 19; // 4080 B .. 1 GiB - 16
+constexpr uint32_t kBigDbl = 11;          // i = 10: A_{1024 * chunk}, the Horner step
+constexpr uint32_t kBigDblWords = kBigChunkClasses * kBigDbl * 128;
+void build_big_dbl(uint32_t *tab /* kBigDblWords */);
 size_t big_route_workspace_bytes(uint64_t n);
 BigRoute big_route_carve(void *ws, uint64_t n);
 // Before the rows pass: flags and lists the big bodies (route.routed goes into

@@ -673,25 +673,21 @@ __device__ __forceinline__ uint32_t nib_map(const uint32_t *m, uint32_t v) {
   for (uint32_t i = 0; i < 8; ++i) r ^= m[i * 16u + ((v >> (4u * i)) & 15u)];
   return r;
 }
-constexpr uint32_t kBigDbl = 11; // A_{chunk * 2^i}, i = 0..10 (i = 10: the Horner step)
 __global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengths, BigRoute r, const uint4 *shift_nib,
                                                            uint32_t *out) {
-  __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
+  constexpr uint32_t kHiMaps = 20;                // A_{2^k}, k = 12..31: the seed's shift by len0 & ~4095
+  __shared__ uint32_t nibhi[kHiMaps * 128];
   __shared__ uint32_t part[16];
-  __shared__ uint32_t dbl[kBigDbl * 128]; // [i][n][j] = A_{chunk * 2^i}(j << 4n)
+  __shared__ uint32_t dbl[kBigDbl * 128];         // [i][n][j] = A_{chunk * 2^i}(j << 4n), the chunk's class
   const uint64_t nb = big_count(r);
   if (blockIdx.x >= nb) return;
   const uint32_t t = threadIdx.x;
-  {
-    uint4 *dst = reinterpret_cast<uint4 *>(nib);
-#pragma unroll
-    for (uint32_t q = 0; q < kShiftNibWords / 4 / 1024; ++q) dst[q * 1024 + t] = shift_nib[q * 1024 + t];
-  }
-  __syncthreads();
   const uint64_t chunk = r.meta[3];
-  for (uint32_t e = t; e < kBigDbl * 128; e += 1024) {
-    const uint32_t i = e >> 7, x = e & 127u;
-    dbl[e] = nib_shift(nib, chunk << i, (x & 15u) << (4u * (x >> 4)));
+  const uint32_t m = (uint32_t)__builtin_ctzll((chunk + 16) >> 12); // chunk = 4096 * 2^m - 16
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(shift_nib) + 12u * 128u;
+    for (uint32_t e = t; e < kHiMaps * 128; e += 1024) nibhi[e] = src[e];
+    for (uint32_t e = t; e < kBigDbl * 128; e += 1024) dbl[e] = r.dbl[m * kBigDbl * 128 + e];
   }
   __syncthreads();
   const uint32_t *stepnib = dbl + 10 * 128; // A_{1024 * chunk}
@@ -699,13 +695,24 @@ __global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengt
     const uint32_t i = big_body(r, b);
     const uint64_t L = lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first;
     uint32_t acc = 0;
-    for (uint64_t k = t; k < nch; k += 1024) {
-      uint32_t raw = r.c_raw[first + k];
-      if (k == 0) { // zlib's pre-conditioning, carried from the body's first byte
-        const uint64_t len0 = L - (nch - 1) * chunk;
-        raw ^= (len0 < kTqEntries) ? r.tq[len0] : nib_shift(nib, len0, 0xFFFFFFFFu);
-      }
-      acc = nib_map(stepnib, acc) ^ raw;
+    // zlib's pre-conditioning, carried in from the body's first byte by chunk 0
+    // (thread 0): A_{len0}(F) = A_{4096 q}(Tq[len0 mod 4096]), one map for q = 1
+    uint32_t seed = 0;
+    if (t == 0 && nch != 0) {
+      const uint64_t len0 = L - (nch - 1) * chunk;
+      seed = r.tq[len0 & 4095u];
+      for (uint64_t q = len0 >> 12; q; q &= q - 1) seed = nib_map(nibhi + 128u * (uint32_t)__builtin_ctzll(q), seed);
+    }
+    // The thread's raw CRCs are loaded kB at a time ahead of the Horner chain
+    // (one dependent global load per step left the fold latency-bound).
+    constexpr uint32_t kB = 8;
+    for (uint64_t k0 = t; k0 < nch; k0 += (uint64_t)kB * 1024u) {
+      uint32_t rv[kB];
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) rv[q] = (k0 + q * 1024u < nch) ? r.c_raw[first + k0 + q * 1024u] : 0u;
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q)
+        if (k0 + q * 1024u < nch) acc = nib_map(stepnib, acc) ^ rv[q] ^ (k0 + q == 0 ? seed : 0u);
     }
     if (t < nch) {
       uint32_t j = (uint32_t)((nch - 1 - t) % 1024u); // chunks after this thread's last one
@@ -780,12 +787,14 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
   a.big_min = 0xFFFFFFFFu;
   a.mode = kModeRaw;
   a.out = r.c_raw;
-  // One-row chunks (4080 B): the tail is dealt from the steal counter, the
+  // Two-row chunks (8176 B): the tail is dealt from the steal counter, the
   // pool sized in the kernel from the device count (crc32_rows.h steal_s).
   a.steal = steal;
   e = launch_rows(a, 1, nt, max_blocks, s, steal_done, steal_recorded);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(big_combine_kernel, dim3(256), dim3(1024), 0, s, proto.lengths, r, shift_nib, proto.out);
+  // 1024 blocks (blocks past the routed-body count leave at once): a block folds
+  // one body at a time, so the count bounds the serial bodies per block.
+  hipLaunchKernelGGL(big_combine_kernel, dim3(1024), dim3(1024), 0, s, proto.lengths, r, shift_nib, proto.out);
   return hipGetLastError();
 }
 

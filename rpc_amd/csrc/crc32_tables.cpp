@@ -1,6 +1,7 @@
 // rpc_amd/csrc/crc32_tables.cpp -- builds the LDS image and the Tq table once
 // per device context (host code; uploaded to HBM, copied to LDS per workgroup).
 #include "crc32_gf2.h"
+#include "crc32_kernels.h"
 #include "crc32_layout.h"
 
 #include <string.h>
@@ -62,6 +63,16 @@ void build_lds_image_v2(uint32_t *img) {
     for (uint32_t n = 0; n < 8; ++n)
       for (uint32_t nib = 0; nib < 16; ++nib) put(sq_byte(j, n, nib), nt[n][nib]);
   }
+}
+
+void build_big_dbl(uint32_t *tab) {
+  for (uint32_t m = 0; m < kBigChunkClasses; ++m)
+    for (uint32_t i = 0; i < kBigDbl; ++i) {
+      const uint64_t nbytes = ((4096ull << m) - 16) << i;
+      const uint32_t xp = gf2_xpow(8ull * nbytes);
+      for (uint32_t n = 0; n < 8; ++n)
+        for (uint32_t j = 0; j < 16; ++j) tab[(m * kBigDbl + i) * 128 + n * 16 + j] = gf2_mulmod(xp, j << (4 * n));
+    }
 }
 
 void build_scalar_tab(uint32_t *tab) {

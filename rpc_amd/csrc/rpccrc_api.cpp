@@ -297,6 +297,7 @@ struct DeviceCtx {
   uint4 *img = nullptr; // LDS table image (rows kernel layout, 155 KiB)
   uint32_t *tq = nullptr;
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
+  uint32_t *big_dbl = nullptr; // the big-body fold's doubling maps per chunk class (build_big_dbl)
   uint4 *scalar_tab = nullptr; // one-wave scalar kernel's table image (kScalarTabWords)
   // Device error word (pinned, coherent host memory): the rows kernel stores
   // kErr* here when a bounded wait runs out (crc32_rows.h).  Sticky: once it is
@@ -350,14 +351,14 @@ uint32_t big_min_for(uint64_t n) {
   return n <= kBigMaxBodies ? kBigMinSmallBatch : kBigMin;
 }
 // Chunk size the route starts from (it grows as (c + 16) * 2 - 16 until the
-// chunks fit kBigMaxChunks): 4080-byte one-row chunks deal with tail stealing
+// chunks fit kBigMaxChunks): 8176-byte two-row chunks deal with tail stealing
 // (launch_rows, device-counted).  Tuning override: RPCCRC_BIG_CHUNK
 // (2^k * 4096 - 16 bytes, e.g. 16368).
 const uint32_t g_big_chunk = [] {
   const char *e = getenv("RPCCRC_BIG_CHUNK");
   const unsigned long long v = e ? strtoull(e, nullptr, 10) : 0ull;
   const unsigned long long p = v + 16;
-  return (v >= kBigMinChunk && p <= (1ull << 30) && (p & (p - 1)) == 0) ? (uint32_t)v : (uint32_t)kBigMinChunk;
+  return (v >= 4096 - 16 && p <= (1ull << 30) && (p & (p - 1)) == 0) ? (uint32_t)v : (uint32_t)kBigMinChunk;
 }();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kSplitMinFrames = 16384;       // fewer frames: one wave per body (rows kernel)
@@ -408,6 +409,7 @@ void init_device(int dev) {
   e = (e == hipSuccess) ? hipMalloc(&c.img, kLdsBytesV3) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.big_dbl, kBigDblWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.scalar_tab, kScalarTabWords * 4) : e;
   e = (e == hipSuccess) ? hipHostMalloc(reinterpret_cast<void **>(&c.err), 64, hipHostMallocCoherent) : e;
   if (e == hipSuccess) *reinterpret_cast<volatile uint32_t *>(c.err) = 0;
@@ -417,6 +419,11 @@ void init_device(int dev) {
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    std::vector<uint32_t> dbl(kBigDblWords);
+    build_big_dbl(dbl.data());
+    e = hipMemcpy(c.big_dbl, dbl.data(), kBigDblWords * 4, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMemcpy(c.scalar_tab, stab.data(), kScalarTabWords * 4, hipMemcpyHostToDevice);
   (void)hipSetDevice(prev);
   c.ws = new BlockPool(false, 1ull << 30);
@@ -525,6 +532,15 @@ struct StealLease {
   hipEvent_t done_event() const { return steal_ext_event() && slot ? slot->ev : nullptr; }
 };
 
+// Tail stealing for ragged rows passes (off: round 2 measured C2 +0.7 %).
+bool ragged_steal() {
+  static const bool v = [] {
+    const char *e = getenv("RPCCRC_RAGGED_STEAL");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
           uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
   ItemsArgs a = items_args(c, base, offsets, lengths, n, stride, len, mode, out);
@@ -600,6 +616,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     r = big_route_carve(ws.ptr() + split_bytes, n);
     r.min_chunk = g_big_chunk;
     r.tq = c.tq;
+    r.dbl = c.big_dbl;
     if (route_all) {
       r.all_n = (uint32_t)n;
     } else {
@@ -613,10 +630,16 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     sl.pool = c.steal;
     sl.s = s;
   }
+  StealLease rsl; // RPCCRC_RAGGED_STEAL=1: the plain rows pass deals its tail from a steal counter too
   if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
   } else if (!route_all) {
-    RPCCRC_TRY(launch_rows(a, 1, nt, mb, s));
+    if (ragged_steal()) {
+      if (const int rc = rsl.get(c, n, 1, s)) return rc;
+      a.steal = rsl.p;
+    }
+    RPCCRC_TRY(launch_rows(a, 1, nt, mb, s, rsl.done_event(), &rsl.recorded));
+    a.steal = nullptr;
   }
   if (route) RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s, sl.p, sl.done_event(), &sl.recorded));
   return RPCCRC_OK;

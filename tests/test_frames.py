@@ -233,11 +233,12 @@ def test_frames_lifted_cap_large_bodies(frames_path):
 def test_frames_lifted_cap_route_all_mixed(role):
     """A small lifted-cap batch (route-all: every body through the chunk route, no
     classify or plain rows pass) with every verdict the parse decides: heartbeats of
-    both types, empty bodies, a bad CRC, bodies around the 4080-byte chunk and the
+    both types, empty bodies, a bad CRC, bodies around the 8176-byte chunk and the
     4096-entry Tq seed table, a header whose body runs past the stream."""
     rng = np.random.default_rng(23 if role == "server" else 24)
     frames = []
-    for L in [0, 1, 15, 16, 1024, 1025, 4079, 4080, 4081, 4096, 4097, 8160, 8161, 20000, 300000, 0, 77]:
+    for L in [0, 1, 15, 16, 1024, 1025, 4095, 4096, 4097, 8175, 8176, 8177, 8192, 12289, 16352, 16353, 20000,
+              300000, 0, 77]:
         b = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
         frames.append(header(L, oracle.crc32(np.frombuffer(b, dtype=np.uint8)) if L else 0) + b)
     frames.append(header(0, 0, type_=rpc_amd.RPC_TYPE_PING))
