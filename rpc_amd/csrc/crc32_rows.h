@@ -357,6 +357,10 @@ constexpr bool kRowsPipe = RPCCRC_ROWS_PIPE != 0;
 #define RPCCRC_SUBROWS 1
 #endif
 constexpr bool kSubRows = RPCCRC_SUBROWS != 0;
+#ifndef RPCCRC_SUB_MERGE
+#define RPCCRC_SUB_MERGE 0
+#endif
+constexpr int kSubMerge = RPCCRC_SUB_MERGE;
 
 namespace rows {
 
@@ -1142,6 +1146,25 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // (profiles/r02/r02r_rows_pipeline_ab.txt).
     constexpr bool kPipe = kRowsPipe && RAGGED && !kTwoChains &&
                            (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose)) == 0;
+    // Row C's chain (full / half / quarter row, rows::*_row_segs) and row P's
+    // merge.  kSubMerge 0: P's merge inside each arm (the scheduler overlaps it
+    // with C's chain); 1: before the arms; 2: after them.
+#define RPCCRC_CHAIN_MERGE(cb, ch, pm)                                                   \
+  do {                                                                                   \
+    if constexpr (kSubMerge == 1) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+    if (kSub && c_r == 0 && c_lp <= kQuarter) {                                          \
+      ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
+      if constexpr (kSubMerge == 0) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+    } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
+      ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
+      if constexpr (kSubMerge == 0) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+    } else {                                                                             \
+      transpose(cb);                                                                     \
+      ch = seg_crc(lds, cb, lsel);                                                       \
+      if constexpr (kSubMerge == 0) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+    }                                                                                    \
+    if constexpr (kSubMerge == 2) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+  } while (0)
     if constexpr (DEPTH == 1 && kPipe && kRaggedAhead2) {
       // The pipeline below with loads two rows ahead: one step issues row M's
       // loads while row N's (the row after C) are in flight, chains row C and
@@ -1176,17 +1199,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         fix_row(c_lp, c_z, c_nr, c_r, cb);
         uint32_t ch;
         RowMerge pm;
-        if (kSub && c_r == 0 && c_lp <= kQuarter) {
-          ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);
-          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
-        } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {
-          ch = half_row_segs(lds, cb, lsel, sub_mu);
-          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
-        } else {
-          transpose(cb);
-          ch = seg_crc(lds, cb, lsel);
-          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
-        }
+        RPCCRC_CHAIN_MERGE(cb, ch, pm);
         finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
         publish();
         p_ok = c_ok;
@@ -1249,18 +1262,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         fix_row(c_lp, c_z, c_nr, c_r, cb);
         uint32_t ch;
         RowMerge pm;
-        // (P's merge in each arm: the scheduler overlaps it with C's chain)
-        if (kSub && c_r == 0 && c_lp <= kQuarter) {
-          ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);
-          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
-        } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {
-          ch = half_row_segs(lds, cb, lsel, sub_mu);
-          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
-        } else {
-          transpose(cb);
-          ch = seg_crc(lds, cb, lsel);
-          pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);
-        }
+        RPCCRC_CHAIN_MERGE(cb, ch, pm);
         finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
         publish();
         p_ok = c_ok;
