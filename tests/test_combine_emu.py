@@ -107,3 +107,57 @@ def test_nib_shift_is_zlib_combine():
 def test_combine_matches_zlib(L, chunk, nt, splits):
     body = random.Random(L * 31 + chunk).randbytes(L)
     assert combine_emulated(body, chunk, nt, splits) == zlib.crc32(body)
+
+
+# ---- big-body route fold (big_combine_kernel) --------------
+# crc = ~XOR_k A_{(nch-1-k) chunk}(raw_k) with raw_0 ^= A_{len0}(F) (zlib's
+# pre-conditioning enters with chunk 0: Tq[len0 mod 4096] then one A_{2^k} map per
+# set bit of len0 >> 12); thread t runs Horner over chunks t, t + NT, ... with the
+# step map A_{NT chunk}, then shifts by A_{j chunk}, j = (nch - 1 - t) mod NT, one
+# doubling map A_{chunk 2^i} per set bit of j (the kernel has NT = 1024 and maps
+# i < 10); an empty body folds to 0.
+
+
+def big_fold_emulated(body: bytes, chunk: int, nt: int) -> int:
+    L = len(body)
+    nch = (L + chunk - 1) // chunk
+    if nch == 0:
+        return 0
+    raw = []
+    for k in range(nch):
+        end = L - (nch - 1 - k) * chunk
+        raw.append(crc0(body[max(0, end - chunk):end]))
+    len0 = L - (nch - 1) * chunk
+    seed = nib_shift(len0 & 4095, 0xFFFFFFFF)  # Tq[len0 & 4095]
+    q, k = len0 >> 12, 12
+    while q:
+        if q & 1:
+            seed = nib_apply(k, seed)
+        q >>= 1
+        k += 1
+    dbl = [lambda v, i=i: nib_shift(chunk << i, v) for i in range(nt.bit_length())]
+    out = 0
+    for t in range(nt):
+        acc, kk = 0, t
+        while kk < nch:
+            acc = nib_shift(nt * chunk, acc) ^ raw[kk] ^ (seed if kk == 0 else 0)
+            kk += nt
+        if t < nch:
+            j, i = (nch - 1 - t) % nt, 0
+            while j:
+                if j & 1:
+                    acc = dbl[i](acc)
+                j >>= 1
+                i += 1
+        out ^= acc
+    return ~out & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("L,chunk,nt", [
+    (0, 4080, 8), (1, 4080, 8), (4080, 4080, 8), (4081, 4080, 8), (8176, 8176, 8), (8177, 8176, 4),
+    (9000, 8176, 4), (5 * 8176 + 7, 8176, 2), (40000, 4080, 4), (33000, 16368, 4), (12345, 8176, 1),
+])
+def test_big_fold_matches_zlib(L, chunk, nt):
+    """The route's fold algebra (seeded chunk 0, doubling maps) equals zlib.crc32."""
+    body = random.Random(L * 7 + chunk).randbytes(L)
+    assert big_fold_emulated(body, chunk, nt) == zlib.crc32(body)
