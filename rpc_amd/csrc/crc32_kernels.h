@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc32_layout.h"
+
 namespace rpccrc {
 
 // Output modes of the items kernel.
@@ -91,14 +93,7 @@ struct BigRoute {
   const uint32_t *tq = nullptr;  // Tq[q] = A_q(0xFFFFFFFF): the combine seeds chunk 0 with it
   const uint32_t *dbl = nullptr; // kBigDblWords: the fold's doubling maps per chunk class (build_big_dbl)
 };
-// The fold's maps, built once per device on the host: for chunk class m
-// (chunk = 4096 * 2^m - 16 bytes, m < kBigChunkClasses) and i < kBigDbl,
-// DBL[m][i][n][j] = A_{chunk * 2^i}(j << 4n).  (Round 3 built them in every
-// fold block from the 32 KiB A_{2^k} maps: ~10 us of a 24 us fold.)
-constexpr uint32_t kBigChunkClasses = 19; // 4080 B .. 1 GiB - 16
-constexpr uint32_t kBigDbl = 11;          // i = 10: A_{1024 * chunk}, the Horner step
-constexpr uint32_t kBigDblWords = kBigChunkClasses * kBigDbl * 128;
-void build_big_dbl(uint32_t *tab /* kBigDblWords */);
+// (The fold's doubling maps per chunk class: crc32_layout.h build_big_dbl.)
 size_t big_route_workspace_bytes(uint64_t n);
 BigRoute big_route_carve(void *ws, uint64_t n);
 // Before the rows pass: flags and lists the big bodies (route.routed goes into

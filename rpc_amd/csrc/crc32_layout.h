@@ -78,6 +78,16 @@ void build_lds_image_v2(uint32_t *img /* kLdsBytesV3 bytes: V2 + the SQ tables *
 // Host-side builder (crc32_tables.cpp).
 void build_tq(uint32_t *tq /* kTqEntries */);
 
+// The big-body route fold's maps (crc32_kernels.hip big_combine_kernel), built
+// once per device on the host: for chunk class m (chunk = 4096 * 2^m - 16
+// bytes, m < kBigChunkClasses) and i < kBigDbl,
+// DBL[m][i][n][j] = A_{chunk * 2^i}(j << 4n).  (Round 3 first built them in every
+// fold block from the 32 KiB A_{2^k} maps: ~10 us of a 24 us fold.)
+constexpr uint32_t kBigChunkClasses = 19; // 4080 B .. 1 GiB - 16
+constexpr uint32_t kBigDbl = 11;          // i = 10: A_{1024 * chunk}, the Horner step
+constexpr uint32_t kBigDblWords = kBigChunkClasses * kBigDbl * 128;
+void build_big_dbl(uint32_t *tab /* kBigDblWords */);
+
 // One-wave scalar kernel (crc32_scalar.hip): bodies of <= kScalarMaxLen
 // bytes.  Table image of kScalarTabWords words: T_k[256] slice-by-4 tables,
 // k = 0..3, then NIB[k - kScalarNibK0][i][j] = A_{2^k bytes}(j << 4i) for

@@ -1,7 +1,6 @@
 // rpc_amd/csrc/crc32_tables.cpp -- builds the LDS image and the Tq table once
 // per device context (host code; uploaded to HBM, copied to LDS per workgroup).
 #include "crc32_gf2.h"
-#include "crc32_kernels.h"
 #include "crc32_layout.h"
 
 #include <string.h>
