@@ -357,10 +357,6 @@ constexpr bool kRowsPipe = RPCCRC_ROWS_PIPE != 0;
 #define RPCCRC_SUBROWS 1
 #endif
 constexpr bool kSubRows = RPCCRC_SUBROWS != 0;
-#ifndef RPCCRC_SUB_MERGE
-#define RPCCRC_SUB_MERGE 0
-#endif
-constexpr int kSubMerge = RPCCRC_SUB_MERGE;
 
 namespace rows {
 
@@ -1147,23 +1143,21 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     constexpr bool kPipe = kRowsPipe && RAGGED && !kTwoChains &&
                            (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose)) == 0;
     // Row C's chain (full / half / quarter row, rows::*_row_segs) and row P's
-    // merge.  kSubMerge 0: P's merge inside each arm (the scheduler overlaps it
-    // with C's chain); 1: before the arms; 2: after them.
+    // merge, inside each arm so the scheduler overlaps it with C's chain (P's
+    // merge before or after the arms measured the same, profiles/r03g).
 #define RPCCRC_CHAIN_MERGE(cb, ch, pm)                                                   \
   do {                                                                                   \
-    if constexpr (kSubMerge == 1) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
     if (kSub && c_r == 0 && c_lp <= kQuarter) {                                          \
       ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
-      if constexpr (kSubMerge == 0) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+      pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
     } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
       ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
-      if constexpr (kSubMerge == 0) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+      pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
     } else {                                                                             \
       transpose(cb);                                                                     \
       ch = seg_crc(lds, cb, lsel);                                                       \
-      if constexpr (kSubMerge == 0) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
+      pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
     }                                                                                    \
-    if constexpr (kSubMerge == 2) pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl); \
   } while (0)
     if constexpr (DEPTH == 1 && kPipe && kRaggedAhead2) {
       // The pipeline below with loads two rows ahead: one step issues row M's
