@@ -352,7 +352,8 @@ constexpr int kRowsAblNoSub = 16384; // ragged QB = 1 without the quarter / half
 #define RPCCRC_ROWS_PIPE 1
 #endif
 constexpr bool kRowsPipe = RPCCRC_ROWS_PIPE != 0;
-// Ragged QB = 1: first rows of <= 1 / 2 KiB as quarter / half rows (rows::sub_chain).
+// Ragged QB = 1: first rows of <= 1 / 2 KiB as quarter / half rows (rows::quarter_row_segs,
+// rows::half_row_segs).
 #ifndef RPCCRC_SUBROWS
 #define RPCCRC_SUBROWS 1
 #endif
@@ -1144,7 +1145,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
                            (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose)) == 0;
     // Row C's chain (full / half / quarter row, rows::*_row_segs) and row P's
     // merge, inside each arm so the scheduler overlaps it with C's chain (P's
-    // merge before or after the arms measured the same, profiles/r03g).
+    // merge before or after the arms: C2 +1.3 % with the max-ilp scheduler,
+    // profiles/r03m).
 #define RPCCRC_CHAIN_MERGE(cb, ch, pm)                                                   \
   do {                                                                                   \
     if (kSub && c_r == 0 && c_lp <= kQuarter) {                                          \

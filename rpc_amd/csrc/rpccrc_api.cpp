@@ -532,7 +532,8 @@ struct StealLease {
   hipEvent_t done_event() const { return steal_ext_event() && slot ? slot->ev : nullptr; }
 };
 
-// Tail stealing for ragged rows passes (off: round 2 measured C2 +0.7 %).
+// Tail stealing for ragged rows passes (off: C2 +0.7 % in round 2, +2.3 % in
+// round 3 with a 15 % or 5 % pool, profiles/r03e/c2_ragged_steal_ab.txt).
 bool ragged_steal() {
   static const bool v = [] {
     const char *e = getenv("RPCCRC_RAGGED_STEAL");
@@ -609,7 +610,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   // every body through the chunk route (no classify pass and no plain rows
   // pass, whose longest non-routed body -- up to the 16 KiB small-batch
   // threshold, one wave -- set its duration: 15 us of a 1024-frame verify).
-  // Bounded because the fold spends a block-wide reduction per body (256
+  // Bounded because the fold spends a block-wide reduction per body (1024
   // blocks): a few bodies per block cost less than the passes they replace.
   const bool route_all = route && small_bodies && !split && n <= kRouteAllMax && !g_big_min_env;
   if (route) {
