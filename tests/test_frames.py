@@ -251,6 +251,25 @@ def test_frames_lifted_cap_route_all_mixed(role):
     assert got == expected(blob, offs, role=role, lift_cap=True)
 
 
+@pytest.mark.parametrize("n", [2048, 2049])
+def test_frames_lifted_cap_route_modes(n):
+    """Lifted-cap batches at the route-all bound (2048 frames: every body through the
+    chunk route) and one past it (2049: classify, plain rows pass for bodies under the
+    16 KiB small-batch threshold, chunk route for the rest): same verdicts and CRCs."""
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 3000, n)
+    lens[::97] = rng.integers(16 << 10, 300 << 10, len(lens[::97]))
+    lens[5] = 0
+    frames = []
+    for i, L in enumerate(lens.tolist()):
+        b = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        c = oracle.crc32(np.frombuffer(b, dtype=np.uint8)) if L else 0
+        frames.append(header(L, c ^ (1 if i % 211 == 7 else 0)) + b)
+    blob, offs = layout(frames)
+    got = verify(blob, offs, lift_cap=True)
+    assert got == expected(blob, offs, lift_cap=True)
+
+
 def test_frames_role_flags_rejected():
     d = to_dev(np.zeros(64, dtype=np.uint8))
     o = to_dev(np.zeros(1, dtype=np.int64))
