@@ -771,6 +771,11 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
                             hipStream_t s, uint32_t *steal, hipEvent_t steal_done, bool *steal_recorded) {
   if (proto.n_items == 0) return hipSuccess;
   if (proto.mode != kModeFinal || proto.offsets == nullptr || proto.lengths == nullptr) return hipErrorInvalidValue;
+  // The fold indexes its maps by chunk class: chunk = 4096 * 2^m - 16 (the plan
+  // only doubles it), m < kBigChunkClasses; r.dbl / r.tq must be set.
+  const uint64_t p = r.min_chunk + 16;
+  if (p < 4096 || (p & (p - 1)) != 0 || (p >> 12) >= (1ull << kBigChunkClasses) || !r.dbl || !r.tq)
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(big_plan_kernel, dim3(1), dim3(1024), 0, s, proto.lengths, r);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
