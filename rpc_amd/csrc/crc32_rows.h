@@ -358,6 +358,13 @@ constexpr bool kRowsPipe = RPCCRC_ROWS_PIPE != 0;
 #define RPCCRC_SUBROWS 1
 #endif
 constexpr bool kSubRows = RPCCRC_SUBROWS != 0;
+// Ragged QB = 1 pipeline: Horner across a body's rows per lane (rows::rw_map)
+// and one merge per body, instead of a merge and a scalar Horner step per row.
+// C2 -0.5 % on two boxes (profiles/r03o, r03p).
+#ifndef RPCCRC_LANE_HORNER
+#define RPCCRC_LANE_HORNER 1
+#endif
+constexpr bool kLaneHorner = RPCCRC_LANE_HORNER != 0;
 
 namespace rows {
 
@@ -485,6 +492,22 @@ __device__ __forceinline__ uint32_t half_row_segs(const uint8_t *lds, u32x4 (&p)
   const uint32_t a = sq_map(lds, c, 0x40404040u); // j = 1: A_32
   auto w = __builtin_amdgcn_permlane32_swap(0u, a, false, false); // w[0]: upper lanes <- a of lower lanes
   return __builtin_amdgcn_bitop3_b32(c, mU, w[0], 0x6A);          // (c & mU) ^ w
+}
+
+// Per-lane A_4096 (lane Horner, kLaneHorner): each lane advances its own
+// segment accumulator by one row, from the single-copy RW table ([n][nib] at
+// kLdsRW2 + n*64 + nib*4: the 16 words of one n sit on 16 banks, lanes with
+// equal nibbles share a word).  One v_perm_b32 per address, n in the immediate.
+__device__ __forceinline__ uint32_t rw_map(const uint8_t *lds, uint32_t s) {
+  static_assert((kLdsRW2 & 255u) == 0, "RW must be 256-B aligned for the perm-formed address");
+  const uint32_t xl4 = (s << 2) & 0x3C3C3C3Cu, xh4 = (s >> 2) & 0x3C3C3C3Cu;
+  uint32_t t[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    t[2 * k] = lds_ld(lds, __builtin_amdgcn_perm(xl4, kLdsRW2, 0x0C020104u + k) + k * 128u);
+    t[2 * k + 1] = lds_ld(lds, __builtin_amdgcn_perm(xh4, kLdsRW2, 0x0C020104u + k) + k * 128u + 64u);
+  }
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 
 struct QuarterInfo {
@@ -1161,6 +1184,45 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
     }                                                                                    \
   } while (0)
+    // Lane Horner (kLH): C's chain only, then row P joins its body's per-lane
+    // accumulator (A_4096 on every row but the first; zlib's seed enters in
+    // lane 63, whose merge shift is A_0), and the body's last row is merged
+    // once: crc0(body) = XOR_L' A_{64(63-L')}(acc_L').
+    constexpr bool kLH = kLaneHorner && kSub;
+    uint32_t lacc = 0; // kLH: this wave's per-lane accumulator of row P's body
+    // (row P's lane-Horner step after C's arms: inside each arm measured
+    // -0.2 % against -0.5 % here, profiles/r03p)
+#define RPCCRC_CHAIN_ONLY(cb, ch)                                                        \
+  do {                                                                                   \
+    if (kSub && c_r == 0 && c_lp <= kQuarter) {                                          \
+      ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
+    } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
+      ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
+    } else {                                                                             \
+      transpose(cb);                                                                     \
+      ch = seg_crc(lds, cb, lsel);                                                       \
+    }                                                                                    \
+    lane_horner_p(p_ok, p_z, p_nr, p_r, p_seed, p_c, p_item, p_chain);                   \
+  } while (0)
+    auto lane_horner_p = [&](bool ok, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed, uint32_t cidx,
+                             uint32_t tsk, uint32_t chain) {
+      if (r != 0) {
+        lacc = rw_map(lds, lacc) ^ chain;
+      } else { // a body's first row starts the accumulator (zlib's seed in lane 63)
+        lacc = chain ^ ((lane == 63u) ? seed : 0u);
+      }
+      if (r + 1 == nr) {
+        const RowMerge m = merge_row(lds, merge_lo(lds, lacc, lsel1), 0u, dl);
+        uint32_t res = m.crc;
+        if (z != 0) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
+        if (mode == kModeFinal) res = ~res;
+        if constexpr (DYN) {
+          if (ok) dyn_out(cidx, tsk, res);
+        } else {
+          if (ok) park(res);
+        }
+      }
+    };
     if constexpr (DEPTH == 1 && kPipe && kRaggedAhead2) {
       // The pipeline below with loads two rows ahead: one step issues row M's
       // loads while row N's (the row after C) are in flight, chains row C and
@@ -1194,9 +1256,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, mb);
         fix_row(c_lp, c_z, c_nr, c_r, cb);
         uint32_t ch;
-        RowMerge pm;
-        RPCCRC_CHAIN_MERGE(cb, ch, pm);
-        finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
+        if constexpr (kLH) {
+          RPCCRC_CHAIN_ONLY(cb, ch);
+        } else {
+          RowMerge pm;
+          RPCCRC_CHAIN_MERGE(cb, ch, pm);
+          finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
+        }
         publish();
         p_ok = c_ok;
         p_len = c_len;
@@ -1257,9 +1323,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
         fix_row(c_lp, c_z, c_nr, c_r, cb);
         uint32_t ch;
-        RowMerge pm;
-        RPCCRC_CHAIN_MERGE(cb, ch, pm);
-        finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
+        if constexpr (kLH) {
+          RPCCRC_CHAIN_ONLY(cb, ch);
+        } else {
+          RowMerge pm;
+          RPCCRC_CHAIN_MERGE(cb, ch, pm);
+          finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
+        }
         publish();
         p_ok = c_ok;
         p_len = c_len;

@@ -8,7 +8,8 @@
 //
 // stdin:  QB misalign n  then n lengths; bodies are splitmix bytes (seed 7)
 //         back to back from byte `misalign` of a 16-aligned buffer.  QB = 1 is
-//         the ragged kernel (sub-row first rows), QB = 5 QB = 1 with full rows.
+//         QB = 1 with sub-row first rows, QB = 6 the same with the ragged kernel's
+//         per-lane Horner (one merge per body), QB = 5 QB = 1 with full rows.
 //         QB = 2 is the packed ragged kernel (crc32_packed.h) and reads
 //         "nwaves min_slice max_slices" after n.
 // stdout: one CRC (hex) per body.
@@ -240,6 +241,16 @@ static void sub_chain(Piece P[4][64], bool quarter, Wave v) {
 }
 
 static bool g_subrows = true; // QB code 1: sub-row first rows (the ragged kernel); 5: full rows only
+static bool g_lane_horner = false; // QB code 6: sub-rows + per-lane Horner (RPCCRC_LANE_HORNER)
+static uint32_t rw_map_emu(uint32_t s) {
+  const uint32_t xl4 = (s << 2) & 0x3C3C3C3Cu, xh4 = (s >> 2) & 0x3C3C3C3Cu;
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    r ^= ld(perm(xl4, kLdsRW2, 0x0C020104u + k) + k * 128u);
+    r ^= ld(perm(xh4, kLdsRW2, 0x0C020104u + k) + k * 128u + 64u);
+  }
+  return r;
+}
 
 static void mask_piece(Piece &p, int64_t v, int64_t len) {
   for (int d = 0; d < 4; ++d) {
@@ -279,6 +290,31 @@ static uint32_t emu_qb1(const uint8_t *p0, uint32_t len) {
     const uint32_t hd = r == 0 ? first : 4096u;
     if (g_subrows && !kTwoChains && hd <= 2048u) sub_chain(P, hd <= 1024u, s);
     else row_chain(P, s);
+    if (g_lane_horner) { // per-lane Horner across rows (rw_map), one merge per body
+      static Wave acc;
+      for (int l = 0; l < 64; ++l) {
+        uint32_t a = (r == 0) ? 0u : rw_map_emu(acc[l]);
+        a ^= s[l];
+        if (r == 0 && l == 63) a ^= g_tq[first];
+        acc[l] = a;
+      }
+      if (!last) continue;
+      for (int l = 0; l < 64; ++l) s[l] = acc[l];
+      merge_lo(s);
+      Wave t;
+      for (int l = 0; l < 64; ++l) {
+        const uint32_t lo = l & 15, hi = l >> 4;
+        const bool own = lo < 8;
+        const uint32_t base = own ? st2_byte(lo, 0u, hi) : kLdsZero;
+        const uint32_t mul = own ? st2_byte(0u, 1u, 0u) - st2_byte(0u, 0u, 0u) : 0u;
+        t[l] = ld(base + ((s[l] >> (4 * (l & 7))) & 15u) * mul);
+      }
+      dist_reduce8(t);
+      xor_lanebit(t, 4);
+      xor_lanebit(t, 5);
+      W = t[4];
+      continue;
+    }
     merge_lo(s);
     for (int h = 0; h < 4; ++h)
       for (int l = 16 * h; l < 16 * h + 16; ++l)
@@ -606,6 +642,10 @@ int main() {
   for (unsigned long i = 0; i < n; ++i) {
     ptr[i] = buf + off;
     off += lens[i];
+  }
+  if (QB == 6) { // QB = 1, sub-rows, per-lane Horner
+    QB = 1;
+    g_lane_horner = true;
   }
   if (QB == 5) { // QB = 1 with full rows only
     QB = 1;

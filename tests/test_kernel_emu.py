@@ -27,13 +27,14 @@ def rows_emu(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("QB", [1, 5, 4])
+@pytest.mark.parametrize("QB", [1, 5, 6, 4])
 @pytest.mark.parametrize("mis", [0, 1, 3, 4, 8, 15])
 def test_emulated_rows_kernel_matches_oracle(rows_emu, QB, mis):
-    """QB 1: the ragged QB = 1 kernel (quarter / half first rows of <= 1 / 2 KiB);
-    QB 5: QB = 1 with full rows only (uniform batches); QB 4: four bodies per row."""
+    """QB 1: QB = 1 with quarter / half first rows of <= 1 / 2 KiB; QB 6: the same with
+    the ragged kernel's per-lane Horner (one merge per body); QB 5: QB = 1 with full
+    rows only (uniform batches); QB 4: four bodies per row."""
     rng = np.random.default_rng(QB * 100 + mis)
-    if QB in (1, 5):
+    if QB in (1, 5, 6):
         lens = (LENS + [1008, 1009, 1010, 1020, 2032, 2033, 2047, 2048, 2049, 2064, 4096 + 1008, 4096 + 2040,
                         8192 + 1500] + rng.integers(0, 20000, 6).tolist() + rng.integers(0, 2100, 12).tolist())
     else:  # QB=4 precondition: len + pad-to-16 <= 1024
