@@ -21,4 +21,18 @@ RPCCRC_HD uint32_t keep_dword(uint32_t lo, uint32_t hi, uint32_t d) {
   return e > s ? (uint32_t)(((1ull << (8u * e)) - 1u) & ~((1ull << (8u * s)) - 1u)) : 0u;
 }
 
+// The two masks the kernels use, with fewer scalar ops than keep_dword (~4 per
+// dword: one clamped shift amount and one 64-bit shift, whose low half is 0
+// for a shift of 32):
+//   keep_front_dword(f, d) == keep_dword(f, 16, d)      (bytes >= f kept, f < 16)
+//   keep_end_dword(k, d)   == keep_dword(0, k, d)       (bytes <  k kept, k <= 16)
+RPCCRC_HD uint32_t keep_front_dword(uint32_t f, uint32_t d) {
+  const int32_t t = (int32_t)(8u * f) - (int32_t)(32u * d); // foreign bits at the dword's low end
+  return t <= 0 ? 0xFFFFFFFFu : (t >= 32 ? 0u : 0xFFFFFFFFu << (uint32_t)t);
+}
+RPCCRC_HD uint32_t keep_end_dword(uint32_t k, uint32_t d) {
+  const int32_t t = (int32_t)(32u * d + 32u) - (int32_t)(8u * k); // foreign bits at the dword's high end
+  return t <= 0 ? 0xFFFFFFFFu : (t >= 32 ? 0u : 0xFFFFFFFFu >> (uint32_t)t);
+}
+
 } // namespace rpccrc

@@ -162,12 +162,12 @@ __device__ __forceinline__ void fix_quarter(u32x4 &x, uint32_t lane, uint32_t fr
     const uint32_t e = (lane == lane_of(front >> 4)) ? 0u : 0xFFFFFFFFu;
     const uint32_t f = front & 15u;
 #pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) x[d] = and_or_keep(x[d], keep_dword(f, 16u, d), e);
+    for (uint32_t d = 0; d < 4; ++d) x[d] = and_or_keep(x[d], keep_front_dword(f, d), e);
   }
   if (z != 0u) {
     const uint32_t e = (lane == lane_of(63u)) ? 0u : 0xFFFFFFFFu;
 #pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) x[d] = and_or_keep(x[d], keep_dword(0u, 16u - z, d), e);
+    for (uint32_t d = 0; d < 4; ++d) x[d] = and_or_keep(x[d], keep_end_dword(16u - z, d), e);
   }
 }
 

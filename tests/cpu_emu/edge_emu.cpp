@@ -13,6 +13,19 @@
 using namespace rpccrc;
 
 int main() {
+  // the kernels' cheaper mask forms equal the general keep_dword
+  for (uint32_t f = 0; f < 16; ++f)
+    for (uint32_t d = 0; d < 4; ++d)
+      if (keep_front_dword(f, d) != keep_dword(f, 16u, d)) {
+        printf("keep_front_dword(%u, %u) %08x != %08x\n", f, d, keep_front_dword(f, d), keep_dword(f, 16u, d));
+        return 1;
+      }
+  for (uint32_t k = 0; k <= 16; ++k)
+    for (uint32_t d = 0; d < 4; ++d)
+      if (keep_end_dword(k, d) != keep_dword(0u, k, d)) {
+        printf("keep_end_dword(%u, %u) %08x != %08x\n", k, d, keep_end_dword(k, d), keep_dword(0u, k, d));
+        return 1;
+      }
   uint8_t mem[1024];
   for (int i = 0; i < 1024; ++i) mem[i] = (uint8_t)(i * 37 + 11) | 1u; // no zero bytes
   long cases = 0;
@@ -33,9 +46,9 @@ int main() {
       // the fix (same steps as fix_quarter, lane-parallel)
       for (uint32_t L = 0; L < 64; ++L) {
         if ((front & 15u) != 0u && front < 1024u && L == lane_of_piece(front >> 4))
-          for (uint32_t d = 0; d < 4; ++d) piece[L][d] &= keep_dword(front & 15u, 16u, d);
+          for (uint32_t d = 0; d < 4; ++d) piece[L][d] &= keep_front_dword(front & 15u, d);
         if (z != 0u && L == lane_of_piece(63u))
-          for (uint32_t d = 0; d < 4; ++d) piece[L][d] &= keep_dword(0u, 16u - z, d);
+          for (uint32_t d = 0; d < 4; ++d) piece[L][d] &= keep_end_dword(16u - z, d);
       }
       for (uint32_t L = 0; L < 64; ++L) {
         const uint32_t p = piece_of_lane(L);
