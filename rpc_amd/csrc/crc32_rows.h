@@ -934,10 +934,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       }
       p0 = (uint64_t)(uintptr_t)a.base + off;
       z = (uint32_t)(0u - (uint32_t)(p0 + len)) & 15u;
-      const uint64_t lp = (uint64_t)len + z;
-      const uint64_t rows_ = (lp + kRow - 1) / kRow;
-      nr = rows_ ? (uint32_t)rows_ : 1u; // zero-length items: one fully masked row
-      hd = (uint32_t)(lp - (uint64_t)(nr - 1) * kRow);
+      // rows and first-row bytes of lp = len + z in 32-bit scalar ops (lp may
+      // pass 2^32): lp = 4096 a + b with b <= 4110, so the rows are a + cb,
+      // cb = ceil(b / 4096) in {0, 1, 2}, and hd = b + 4096 (1 - cb)
+      const uint32_t ra = len >> 12, rb = (len & (kRow - 1u)) + z, cb = (rb + kRow - 1u) >> 12;
+      nr = ra + cb;
+      hd = rb + kRow - cb * kRow;
+      if (nr == 0u) { // zero-length items: one fully masked row
+        nr = 1u;
+        hd = 0u;
+      }
       if constexpr ((ABL & kRowsAblLdsSeed) != 0)
         seed = hd; // resolved in compute
       else
