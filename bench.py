@@ -539,7 +539,9 @@ def main():
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     dist = None
-    if world > 1:
+    # Under torch.distributed.run even one rank joins a process group, so a
+    # one-GPU box runs the N > 1 code path (RCCL barrier and reductions) too.
+    if world > 1 or "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
 
         if args.dist_backend == "nccl":

@@ -196,3 +196,47 @@ def test_gloo_world2_sharded_large_body():
 def test_gloo_world2_sharded_large_body_hip():
     """The same through rpc_crc32_device_large per rank (two ranks on cuda:0)."""
     _run_large(2, on_gpu=True)
+
+
+# ---- the "nccl" (RCCL) backend on hardware -----------------------------------
+# RCCL refuses two ranks on one GPU, and a gpurun box has one, so this runs one
+# rank: the communicator is created on cuda:0 and every collective bench.py and
+# sharded_large_crc issue runs through RCCL on device tensors.
+
+def _rccl_worker(port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        import rpc_amd
+        from oracle import oracle
+        out = {"backend": dist.get_backend(), "barrier": barrier(dist, dev),
+               "max": max_over_ranks(dist, 2.5, dev), "sum": sum_over_ranks(dist, 1 << 40, dev)}
+        length = (5 << 20) + 333
+        x = torch.empty((length + 7) // 8 * 8, dtype=torch.uint8, device=dev)
+        rpc_amd.fill_random(x, 0x5EED0007)
+        lo, hi = large_body_range(length, 0, 1)
+        mine = int(rpc_amd.device_large(x, [lo], [hi - lo]).cpu().numpy().view(np.uint32)[0])
+        out["large"] = sharded_large_crc(dist, mine, hi - lo, device=dev)
+        out["want"] = oracle.crc32(x[:length].cpu().numpy())
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_world1_collectives():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=110)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert out["backend"] == "nccl"
+    assert out["barrier"] == 1 and out["max"] == 2.5 and out["sum"] == 1 << 40
+    assert out["large"] == out["want"]
