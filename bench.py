@@ -406,22 +406,59 @@ def frames_lifted_probe(device, n=1024, reps=5, seed=0x5EED0007):
 
 
 def stream_read_probe(w: Workload, reps=10):
-    """Achievable HBM read rate on the same buffer: a pure streaming read with
-    coalesced 16-B lanes, non-temporal (the CRC kernel's load shape) and
-    temporal.  The rows kernel's ceiling is the nt1 number, not 8 TB/s."""
+    """Achievable HBM read rate on the same buffer (SURVEY 8d "a measured
+    stream-read kernel"):
+      * rows_dealing_GBps -- the ceiling of the product's own memory stream: the
+        rows kernel with its CRC work compiled out, same DYN rounds + tail
+        stealing, same 4 x 16 B non-temporal loads a row ahead, no stores
+        (rpc_crc32_stream_read_device pattern 2).  frac_of_stream_read uses it.
+      * coalesced_nt{1,0}_GBps -- a plain grid-stride loop with coalesced 16-B
+        lanes and no tail dealing (rounds 1-3's probe; the product beat it)."""
     nbytes = (w.total // 4096) * 4096
     stream = torch.cuda.current_stream()
     res = {}
-    for nt in (1, 0):
-        rpc_amd.stream_read(w.base, 0, nontemporal=bool(nt), nbytes=nbytes)
+
+    def timed(fn):
+        fn()
+        t0 = time.perf_counter()  # clock prewarm (DESIGN.md 5)
+        while time.perf_counter() - t0 < 0.2:
+            fn()
+            torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(reps):
-            rpc_amd.stream_read(w.base, 0, nontemporal=bool(nt), nbytes=nbytes)
+            fn()
         e1.record(stream)
         e1.synchronize()
-        res[f"coalesced_nt{nt}_GBps"] = round(nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+        return e0.elapsed_time(e1) / 1e3 / reps
+
+    nrows = min(nbytes, 1 << 34) // 4096  # <= 16 GiB per launch (C2's 37 GiB: its first 16 GiB)
+    if nrows >= (1 << 16):
+        t = timed(lambda: rpc_amd.stream_read(w.base, 2, nbytes=nrows * 4096))
+        res["rows_dealing_GBps"] = round(nrows * 4096 / t / 1e9, 1)
+        res["rows_dealing_us"] = round(t * 1e6, 2)
+    for nt in (1, 0):
+        t = timed(lambda: rpc_amd.stream_read(w.base, 0, nontemporal=bool(nt), nbytes=nbytes))
+        res[f"coalesced_nt{nt}_GBps"] = round(nbytes / t / 1e9, 1)
     return res
+
+
+def unbounded_ragged_us(w: Workload, steps: int) -> float:
+    """Average step of the same ragged batch through rpc_crc32_device_batch (no
+    length bound: the big-body route's classify pass and its passes, empty here, run
+    too), timed like the main line after a short re-warm."""
+    stream = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:
+        rpc_amd.device_batch(w.base, w.offs, w.lens, out=w.out)
+        torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        rpc_amd.device_batch(w.base, w.offs, w.lens, out=w.out)
+    e1.record(stream)
+    e1.synchronize()
+    return round(e0.elapsed_time(e1) * 1e3 / steps, 2)
 
 
 def load_traffic(cfg: str):
@@ -485,6 +522,57 @@ def live_traffic(args, algo_bytes: int):
         "live: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this config (2 x FETCH_SIZE + WRITE_SIZE, KiB)"
 
 
+def rank_timing(dist, device, wall: float, kernel_s: float, median_s: float, total: int):
+    """Per-launch times over ranks ("over the slowest rank").  N = 1:
+    this rank's.  N > 1: the slowest rank's wall time and average / median launch
+    (the roofline reports the slowest rank, as `value` does), the fastest rank's
+    average launch for the spread, and the bytes of all ranks."""
+    if dist is None:
+        return {"wall": wall, "kernel_s": kernel_s, "kernel_min_s": kernel_s, "median_s": median_s, "total": total}
+    from rpc_amd.shard import max_over_ranks, min_over_ranks, sum_over_ranks
+
+    return {"wall": max_over_ranks(dist, wall, device), "kernel_s": max_over_ranks(dist, kernel_s, device),
+            "kernel_min_s": min_over_ranks(dist, kernel_s, device),
+            "median_s": max_over_ranks(dist, median_s, device), "total": sum_over_ranks(dist, total, device)}
+
+
+def roofline_fields(algo_bytes: int, t: dict, world: int) -> dict:
+    """The roofline object's timing part: achieved = one rank's algorithmic bytes
+    per launch / the slowest rank's average launch (ranks carry equal shards)."""
+    achieved = algo_bytes / t["kernel_s"] / 1e9
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_BPS / 1e9,
+        "unit": "GB/s",
+        "frac": round(achieved / (HBM_PEAK_BPS / 1e9), 4),
+        "avg_launch_us": round(t["kernel_s"] * 1e6, 2),
+        "median_launch_us": round(t["median_s"] * 1e6, 2),
+        "per_rank": {"ranks": world, "min_us": round(t["kernel_min_s"] * 1e6, 2),
+                     "max_us": round(t["kernel_s"] * 1e6, 2),
+                     "of": "average launch duration on each rank's kernel stream; achieved/frac use max_us"},
+        "algo_bytes_per_launch": algo_bytes,
+    }
+
+
+def reduce_rehearsal(args, world: int, rank: int):
+    """RPCCRC_BENCH_REDUCE_ONLY (tests/test_bench_launch.py): the N > 1 reductions and
+    the rank-0 roofline fields over gloo on the CPU, with synthetic per-rank launch
+    times (rank r: (1 + r / 10) ms per launch) -- no device work."""
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    k = 1e-3 * (1.0 + rank / 10.0)
+    algo = CONFIGS[args.config][2] * (CONFIGS[args.config][3] + 4)
+    t = rank_timing(dist, None, k * args.steps, k, k, algo - 4 * CONFIGS[args.config][2])
+    if rank == 0:
+        line = {"n_gpus": world, "value": round(t["total"] * args.steps / t["wall"] / GiB, 2),
+                "roofline": roofline_fields(algo, t, world)}
+        sys.stdout.flush()
+        os.write(1, (json.dumps(line) + "\n").encode())
+    dist.destroy_process_group()
+
+
 def free_port() -> int:
     import socket
 
@@ -522,6 +610,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
+    if os.environ.get("RPCCRC_BENCH_REDUCE_ONLY"):  # CPU rehearsal of the N > 1 reductions (gloo)
+        reduce_rehearsal(args, world, rank)
+        return
     if os.environ.get("RPCCRC_BENCH_LAUNCH_ONLY"):  # CPU rehearsal of the launch path (tests/test_bench_launch.py)
         line = json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus,
                            "master": os.environ.get("MASTER_ADDR"), "config": args.config}) + "\n"
@@ -529,7 +620,7 @@ def main():
         os.write(1, line.encode())  # one write(2) < PIPE_BUF: ranks sharing the pipe cannot interleave
         return
     _load_gpu_modules()
-    from rpc_amd.shard import barrier, max_over_ranks, sum_over_ranks
+    from rpc_amd.shard import barrier
 
     if world != args.gpus:
         print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
@@ -603,8 +694,8 @@ def main():
         torch.cuda.synchronize()
         median_s = float(np.median([mev[k].elapsed_time(mev[k + 1]) / 1e3 for k in range(args.steps)]))
         median_src = "second K-step pass with an event after every step (each adds a marker between launches)"
-    tmax = max_over_ranks(dist, wall, device) if dist else wall
-    total_bytes = sum_over_ranks(dist, w.total, device) if dist else w.total
+    tr = rank_timing(dist, device, wall, kernel_s, median_s, w.total)
+    tmax, total_bytes = tr["wall"], tr["total"]
 
     extra = {}
     cpu = None
@@ -617,6 +708,8 @@ def main():
             if w.kind == "uniform":
                 log("receive ring")
                 extra["rx_ring"] = rx_ring_probe()
+        if w.kind == "ragged":  # the plain (unbounded) entry point beside the bounded one
+            extra["unbounded_launch_us"] = unbounded_ragged_us(w, args.steps)
         if w.name == "ns" and not args.no_host_inclusive:
             log("lifted-cap frames (1 B - 64 MiB bodies)")
             extra["frames_lifted"] = frames_lifted_probe(device)
@@ -628,7 +721,7 @@ def main():
             cpu = cpu_baseline(w, args.cpu_seconds)
 
     if rank == 0:
-        achieved = w.algo_bytes / kernel_s / 1e9
+        achieved = w.algo_bytes / tr["kernel_s"] / 1e9
         traffic_rec, traffic_src = None, "not measured"
         if world == 1 and not args.no_live_traffic:
             log("measuring HBM traffic (two rocprofv3 PMC passes)")
@@ -657,16 +750,17 @@ def main():
                 "bodies_per_gpu": w.n,
                 "body_len": w.L if w.kind != "ragged" else "log-uniform 64..65536",
                 "ragged_path": args.ragged_path if w.kind == "ragged" else None,
+                "entry_point": {"uniform": "rpc_crc32_device_uniform",
+                                "ragged": f"rpc_crc32_device_batch_bounded (max_len = {getattr(w, 'max_len', 0)}: "
+                                          "no big-body route passes; extra.unbounded_launch_us times "
+                                          "rpc_crc32_device_batch)",
+                                "large": "rpc_crc32_device_large"}[w.kind],
                 "bytes_per_gpu": w.total,
                 "parallelism": f"dp{world} (payload-index shards, "
                                + ("RCCL barrier only)" if args.dist_backend == "nccl" or world == 1 else "gloo rehearsal barrier)"),
             },
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_BPS / 1e9,
-                "unit": "GB/s",
-                "frac": round(achieved / (HBM_PEAK_BPS / 1e9), 4),
+                **roofline_fields(w.algo_bytes, tr, world),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "traffic_detail": traffic_rec,
@@ -674,17 +768,17 @@ def main():
                            "ragged": "crc32_packed_kernel (+count/scan/plan)" if args.ragged_path == "packed"
                            else "crc32_rows_kernel",
                            "large": "crc32_rows_kernel (+chunk combine)"}[w.kind],
-                "avg_launch_us": round(kernel_s * 1e6, 2),
-                "median_launch_us": round(median_s * 1e6, 2),
                 "median_source": median_src,
-                "algo_bytes_per_launch": w.algo_bytes,
                 # the same achieved rate against a streaming read
-                # of the same buffer on the same GPU (non-temporal, the rows
-                # kernel's load shape), measured in this run.
-                "frac_of_stream_read": (round(achieved / extra["stream_read_probe"]["coalesced_nt1_GBps"], 4)
-                                        if "stream_read_probe" in extra else None),
+                # of the same buffer on the same GPU, measured in this run: the
+                # rows kernel's own dealing and loads with no CRC work
+                # (stream_read_probe rows_dealing_GBps).
+                "frac_of_stream_read": (round(achieved / extra["stream_read_probe"]["rows_dealing_GBps"], 4)
+                                        if "rows_dealing_GBps" in extra.get("stream_read_probe", {}) else None),
             },
-            "cpu_baseline": cpu,
+            # the reference crc.c on the host's cores: timed on rank 0 at N = 1 only
+            # (an N > 1 run shares the host among N ranks)
+            "cpu_baseline": cpu if world == 1 else None,
             "prewarm": {"seconds": args.prewarm_s, "steps": prewarm_steps},
             "device": rpc_amd.device_info(),
             "extra": extra,

@@ -48,7 +48,7 @@ extern "C" {
 #define RPCCRC_ENODEV (-19) /* no usable HIP device */
 #define RPCCRC_ENOMEM (-12) /* device or pinned allocation failed */
 #define RPCCRC_EIO (-5)     /* HIP runtime / kernel launch error, or a kernel-reported
-                               device error (rpc_crc32_device_status) */
+                               error (rpc_crc32_device_status) */
 #define RPCCRC_EAGAIN (-11) /* receive ring: no free segment yet, poll first */
 
 /* ---- drop-in (reference crc.h) ---------------------------------------- */
@@ -76,16 +76,19 @@ RPCCRC_API int64_t rpc_crc32_verify_batch(const uint8_t *base, const uint64_t *o
 
 /* Ragged batch: body i = d_base[d_offsets[i] .. + d_lengths[i]).  All pointers
  * are device pointers on the current device.  Asynchronous on `stream`.
- * Bodies of >= 256 KiB are cut into chunks on the device and folded with the
- * GF(2) combine, so one long body does not serialise the batch on one wave. */
+ * Bodies of >= 256 KiB (>= 16 KiB in batches of <= 16384 bodies) are cut into
+ * chunks on the device and folded with the GF(2) combine, so one long body does
+ * not serialise the batch on one wave. */
 RPCCRC_API int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
                            uint64_t n, uint32_t *d_out, void *stream);
 
 /* rpc_crc32_device_batch with a length bound the caller knows (e.g. MAX_BODY_LEN,
  * rpc.h:17, or a workload's maximum): max_len >= every d_lengths[i], 0 = none.
- * With a bound below 256 KiB the big-body chunk route is never needed and its
- * passes are not launched.  Results never depend on the hint: a body longer
- * than a wrong bound is still CRC'd exactly (by one wavefront, so slowly). */
+ * With a bound below the big-body route threshold the route is never needed
+ * and its passes are not launched.  The threshold depends on the batch size:
+ * 16 KiB for n <= 16384 bodies, 256 KiB above (RPCCRC_BIG_MIN overrides both).
+ * Results never depend on the hint: a body longer than a wrong bound is still
+ * CRC'd exactly (by one wavefront, so slowly). */
 RPCCRC_API int rpc_crc32_device_batch_bounded(const uint8_t *d_base, const uint64_t *d_offsets,
                                               const uint32_t *d_lengths, uint64_t n, uint32_t max_len,
                                               uint32_t *d_out, void *stream);
@@ -229,7 +232,11 @@ RPCCRC_API uint32_t rpc_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len
 RPCCRC_API int rpc_crc32_fill_random_device(void *d_dst, uint64_t nbytes, uint64_t seed, void *stream);
 
 /* HBM read probe over nbytes (multiple of 4096): pattern 0 = coalesced 16-B
- * lanes, 1 = the CRC kernel's 64-B-per-lane segments. */
+ * lanes, 1 = the CRC kernel's 64-B-per-lane segments (both a plain grid-stride
+ * loop), 2 = the rows kernel itself with its CRC work compiled out: the same
+ * dealing (workgroup rounds + tail stealing), loads (4 x 16 B non-temporal per
+ * lane, a row ahead) and launch shape, i.e. the ceiling of the product's memory
+ * stream (nbytes >= 256 MiB on 256 CUs; `nontemporal` is ignored). */
 RPCCRC_API int rpc_crc32_stream_read_device(const void *d_src, uint64_t nbytes, int pattern, int nontemporal, void *stream);
 
 /* Tuning knobs (process-wide): nontemporal loads (0/1, default 1) and the
@@ -258,13 +265,22 @@ RPCCRC_API const char *rpc_crc32_strerror(int err);
 /* Writes "device=<name> arch=<gcn> cus=<n>" for the current device. */
 RPCCRC_API int rpc_crc32_device_info(char *buf, size_t buflen);
 
-/* Sticky device status of the current device: RPCCRC_OK, or RPCCRC_EIO once a
- * kernel has stored into the library's device error word (a bounded wait of the
- * rows kernel's dealing protocol ran out, so CRCs of that launch may be stale).
- * Like a sticky HIP error it stays set for the life of the process, and every
- * later call on the device returns RPCCRC_EIO (the drop-in calls abort).  Device
- * calls are asynchronous: check after synchronising the stream. */
+/* Device error status of the current device: RPCCRC_OK, or RPCCRC_EIO once a
+ * kernel launched by an ASYNCHRONOUS call (device batches, large bodies, frames,
+ * the receive ring) has stored into the device's error word -- a bounded wait of
+ * the rows kernel's dealing protocol ran out (after 30 s), so CRCs of that launch
+ * may be stale.  While it is set, every asynchronous call on the device returns
+ * RPCCRC_EIO.  Device calls are asynchronous: check after synchronising the
+ * stream.  The synchronous calls (rpc_crc32, rpc_crc32_verify, rpc_crc32_batch,
+ * rpc_crc32_verify_batch) report their own launches' errors in their own return
+ * (the drop-in calls abort) and are neither affected by nor recorded in it. */
 RPCCRC_API int rpc_crc32_device_status(void);
+
+/* Clears the current device's error word so asynchronous calls work again, and
+ * returns what rpc_crc32_device_status returned before (RPCCRC_OK or
+ * RPCCRC_EIO).  Call it after synchronising every stream whose results are in
+ * doubt: outputs of the launch that failed are not repaired. */
+RPCCRC_API int rpc_crc32_device_clear_status(void);
 
 #ifdef __cplusplus
 }

@@ -42,6 +42,7 @@ __all__ = [
     "set_ragged_path",
     "device_info",
     "device_status",
+    "device_clear_status",
     "RPC_HEADER_LEN",
     "RPC_TYPE_DATA",
     "RPC_TYPE_PING",
@@ -260,7 +261,8 @@ def fill_random(tensor, seed: int, stream=None):
 
 
 def stream_read(tensor, pattern: int = 0, nontemporal: bool = False, nbytes: Optional[int] = None, stream=None):
-    """HBM read probe (pattern 0 coalesced, 1 = CRC-kernel 64-B lane segments)."""
+    """HBM read probe: pattern 0 coalesced 16-B lanes, 1 = 64-B lane segments (grid-stride
+    loops), 2 = the rows kernel's own dealing and loads with the CRC work compiled out."""
     if nbytes is None:
         nbytes = (tensor.numel() * tensor.element_size()) // 4096 * 4096
     check(_lib.rpc_crc32_stream_read_device(tensor.data_ptr(), nbytes, pattern, int(nontemporal),
@@ -285,8 +287,14 @@ def set_ragged_path(path="auto"):
 
 
 def device_status() -> int:
-    """0, or -5 (RPCCRC_EIO) once a kernel has reported a device error (sticky)."""
+    """0, or -5 (RPCCRC_EIO) once a kernel of an asynchronous call has reported an
+    error into the device's error word (until device_clear_status())."""
     return int(_lib.rpc_crc32_device_status())
+
+
+def device_clear_status() -> int:
+    """Clears the device error word; returns the status it held (0 or -5)."""
+    return int(_lib.rpc_crc32_device_clear_status())
 
 
 def device_info() -> str:

@@ -79,6 +79,7 @@ rpc_crc32_set_ragged_path = _sig("rpc_crc32_set_ragged_path", _i32, _i32)
 rpc_crc32_strerror = _sig("rpc_crc32_strerror", ctypes.c_char_p, _i32)
 rpc_crc32_device_info = _sig("rpc_crc32_device_info", _i32, ctypes.c_char_p, _sz)
 rpc_crc32_device_status = _sig("rpc_crc32_device_status", _i32)
+rpc_crc32_device_clear_status = _sig("rpc_crc32_device_clear_status", _i32)
 
 #: Every symbol include/rpccrc.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -107,6 +108,7 @@ EXPORTS = (
     "rpc_crc32_strerror",
     "rpc_crc32_device_info",
     "rpc_crc32_device_status",
+    "rpc_crc32_device_clear_status",
 )
 
 

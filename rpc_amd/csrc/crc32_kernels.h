@@ -212,5 +212,11 @@ hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes,
 hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream);
 hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool nt, int max_blocks, uint32_t *out,
                               hipStream_t stream);
+// The rows kernel's memory stream alone (uniform 4 KiB rows, DYN + tail
+// stealing from a.steal, CRC work compiled out; a.out: >= 16 * max_blocks words
+// the kernel never stores in practice).  Only for batches large enough to deal
+// dynamically with a steal pool.
+hipError_t launch_stream_rows(const ItemsArgs &a, int max_blocks, hipStream_t stream, hipEvent_t steal_done = nullptr,
+                              bool *steal_recorded = nullptr);
 
 } // namespace rpccrc

@@ -815,6 +815,40 @@ hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipSt
   return hipGetLastError();
 }
 
+// Stream-read probe with the rows kernel's own memory stream (pattern 2): the
+// product kernel (uniform 4 KiB rows, DYN rounds + tail stealing, 4 x 16 B NT
+// buffer loads per lane issued a row ahead, one exit at the bottom) with every
+// CRC instruction compiled out -- no LDS image, no transpose, no chain, no
+// merge, no stores.  This is the ceiling the product's dealing and load shape
+// can reach on the buffer; the plain grid-stride probe above has no tail
+// dealing, and the product beat it.
+constexpr int kStreamRowsAbl = kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblNoStore |
+                               kRowsAblNoImage;
+hipError_t launch_stream_rows(const ItemsArgs &a, int max_blocks, hipStream_t stream, hipEvent_t steal_done,
+                              bool *steal_recorded) {
+  if (a.n_items == 0) return hipSuccess;
+  if (a.offsets != nullptr || a.len != 4096 || a.stride != 4096 || a.n_items > kMaxLaunchItems || a.out == nullptr)
+    return hipErrorInvalidValue;
+  uint64_t blocks = (a.n_items + 15) / 16;
+  if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
+  const uint64_t round = dyn_round(1);
+  if (a.n_items < 8ull * round * blocks || a.steal == nullptr) return hipErrorInvalidValue; // DYN + stealing only
+  ItemsArgs k = a;
+  const uint64_t rounds = (a.n_items + round - 1) / round;
+  const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac())) / blocks;
+  if (!(st >= kStealAhead && st * blocks < rounds)) return hipErrorInvalidValue;
+  k.steal_s = (uint32_t)st;
+  const dim3 grid((unsigned)blocks), block(1024);
+  if (steal_done) {
+    hipExtLaunchKernelGGL((crc32_rows_kernel<1, true, false, kStreamRowsAbl, 1, true, true>), grid, block, 0, stream,
+                          nullptr, steal_done, 0, k);
+    if (steal_recorded) *steal_recorded = true;
+  } else {
+    hipLaunchKernelGGL((crc32_rows_kernel<1, true, false, kStreamRowsAbl, 1, true, true>), grid, block, 0, stream, k);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool nt, int max_blocks, uint32_t *out,
                               hipStream_t stream) {
   const uint64_t ntiles = nbytes / 4096;

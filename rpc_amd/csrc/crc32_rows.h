@@ -583,14 +583,25 @@ constexpr uint32_t kStealAhead = RPCCRC_STEAL_AHEAD;
 constexpr uint32_t kStealQ = 16;                      // LDS queue ring
 constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
 // Bounded waits.  Both waits end by protocol (a claim is published by the wave
-// holding it before that wave waits on anything, and an output-ring slot is
-// freed by the wave finishing its round's last task), so these caps never
-// trigger in a healthy launch.  If one does (~0.1 s of spinning), the wave
-// stores kErrStealWait / kErrRingWait into the device error word a.err and
+// holding it at the end of its current row, before it waits on anything, and
+// an output-ring slot is freed by the wave finishing its round's last task),
+// so these caps never trigger in a healthy launch.  If one does, the wave
+// stores kErrStealWait / kErrRingWait into the launch's error word a.err and
 // moves on -- the host then reports RPCCRC_EIO instead of returning stale CRCs
 // silently (VERDICT / ADVICE r02), and no wait can turn into a hang.
-constexpr uint32_t kStealSpinMax = 1u << 21;
-constexpr uint32_t kRingSpinMax = 1u << 21;
+// The cap is wall time (s_memrealtime, 100 MHz), not a spin count: a ring slot
+// waits for the slowest task of the round 8 rounds back, and one task may be a
+// body of up to 4 GiB walked by ONE wave (a ragged batch whose length bound
+// skips the big-body route) -- ~1-3 s at one wave's rate.  Round 3's cap of
+// 2^21 sleeps (~0.1 s) fired on such a healthy launch.
+constexpr uint64_t kWaitCapTicks = 30ull * 100000000ull; // 30 s
+// Lane 0's wait-loop clock: the first call (spin 0) starts it, later calls
+// report whether the cap has passed.
+__device__ __forceinline__ bool wait_expired(uint32_t spin, uint64_t &t0) {
+  const uint64_t now = __builtin_amdgcn_s_memrealtime();
+  if (spin == 0) t0 = now;
+  return now - t0 > kWaitCapTicks;
+}
 constexpr uint32_t dyn_ring_words(int QB) { return 1 + 2 * dyn_slots(QB) + dyn_slots(QB) * dyn_round(QB) * (uint32_t)QB; }
 constexpr uint32_t dyn_ctl_words(int QB) { return dyn_ring_words(QB) + kStealCtlWords; }
 
@@ -755,8 +766,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   };
   // Lane 0: wait until output-ring slot `slot` is free for round `rnd` (bounded).
   auto ring_wait = [&](const uint32_t *gen, uint32_t slot, uint32_t rnd) {
+    uint64_t t0 = 0;
     for (uint32_t spin = 0; __hip_atomic_load(&gen[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rnd; ++spin) {
-      if (spin >= kRingSpinMax) {
+      if (wait_expired(spin, t0)) {
         report_err(kErrRingWait);
         break;
       }
@@ -811,6 +823,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       more = false;
       return n_tasks;
     }
+    uint64_t t0 = 0;
     for (uint32_t spin = 0;; ++spin) {
       uint32_t st = 0, id = 0;
       if (lane == 0) {
@@ -824,7 +837,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
       if (st == 1u) return ((pool_first + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kRound) | (c % kRound);
       if (st == 2u) break;
-      if (spin >= kStealSpinMax) { // never in a healthy launch: fail loudly, do not hang
+      if (wait_expired(spin, t0)) { // never in a healthy launch: fail loudly, do not hang
         if (lane == 0) report_err(kErrStealWait);
         break;
       }

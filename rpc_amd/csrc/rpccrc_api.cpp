@@ -267,6 +267,10 @@ struct ScalarCtx {
   uint8_t *pin = nullptr;   // pinned input staging, device-readable (zero-copy)
   uint32_t *pout = nullptr; // pinned result (rows kernel path)
   uint64_t *pres = nullptr; // pinned {crc, seq} of the one-wave kernel (polled)
+  // Error word of this context's rows / large-body launches (pinned, coherent:
+  // pres[1]).  A drop-in call checks its own word after its sync, so one failed
+  // launch elsewhere on the device never takes the drop-in calls down with it.
+  uint32_t *perr = nullptr;
   uint32_t seq = 0;
 };
 
@@ -288,6 +292,7 @@ struct HostSlot {
 };
 struct HostPipeline {
   HostSlot slot[2];
+  uint32_t *perr = nullptr; // error word of this call's launches (pinned, coherent)
   bool ok = false;
 };
 
@@ -299,10 +304,14 @@ struct DeviceCtx {
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
   uint32_t *big_dbl = nullptr; // the big-body fold's doubling maps per chunk class (build_big_dbl)
   uint4 *scalar_tab = nullptr; // one-wave scalar kernel's table image (kScalarTabWords)
-  // Device error word (pinned, coherent host memory): the rows kernel stores
-  // kErr* here when a bounded wait runs out (crc32_rows.h).  Sticky: once it is
-  // non-zero every call on this device returns RPCCRC_EIO (the drop-in calls
-  // abort), like a sticky HIP error -- CRCs of the failed launch may be stale.
+  // Device error word (pinned, coherent host memory) of the ASYNCHRONOUS calls
+  // (device batches, large bodies, frames): the rows kernel stores kErr* here
+  // when a bounded wait runs out (crc32_rows.h).  Once it is non-zero, every
+  // asynchronous call on this device returns RPCCRC_EIO until the caller clears
+  // it (rpc_crc32_device_clear_status) -- CRCs of the failed launch may be
+  // stale, and an asynchronous call has no later point at which to report it.
+  // The synchronous calls (drop-in, host batch) use a word of their own per
+  // call and are not affected by it.
   uint32_t *err = nullptr;
   int status = RPCCRC_ENODEV;
   char name[128] = {0};
@@ -434,12 +443,13 @@ void init_device(int dev) {
   c.status = map_hip(e);
 }
 
-// Sticky device error (DeviceCtx::err): RPCCRC_EIO once a kernel has reported one.
-int device_error(const DeviceCtx &c) {
-  return (c.err != nullptr && *reinterpret_cast<const volatile uint32_t *>(c.err) != 0u) ? RPCCRC_EIO : RPCCRC_OK;
+// A kernel-reported error in the word w (a device's or a call's own).
+int word_error(const uint32_t *w) {
+  return (w != nullptr && *reinterpret_cast<const volatile uint32_t *>(w) != 0u) ? RPCCRC_EIO : RPCCRC_OK;
 }
+int device_error(const DeviceCtx &c) { return word_error(c.err); }
 
-// Context of the calling thread's current device.
+// Context of the calling thread's current device (its initialisation status).
 int get_ctx(DeviceCtx **out) {
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return RPCCRC_ENODEV;
@@ -447,18 +457,30 @@ int get_ctx(DeviceCtx **out) {
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RPCCRC_ENODEV;
   std::call_once(g_once[dev], init_device, dev);
   *out = &g_dev[dev];
-  if (g_dev[dev].status != RPCCRC_OK) return g_dev[dev].status;
-  return device_error(g_dev[dev]);
+  return g_dev[dev].status;
 }
 
-// Test-only: RPCCRC_TEST_STEAL_GIVEUP=1 makes every tail-stealing pool-round
-// wait give up (ItemsArgs.test_giveup), to exercise the device error word.
-uint32_t test_giveup() {
-  static const uint32_t v = [] {
+// The same for an asynchronous call: RPCCRC_EIO while the device error word
+// holds an uncleared error (DeviceCtx::err).
+int get_async_ctx(DeviceCtx **out) {
+  const int rc = get_ctx(out);
+  return rc ? rc : device_error(**out);
+}
+
+// Test hook, compiled into the test build only (librpccrc_test.so,
+// -DRPCCRC_TEST_HOOKS; ADVICE r03: the shipping library must not read it):
+// RPCCRC_TEST_STEAL_GIVEUP=K makes the next K tail-stealing launches give up
+// every pool-round wait (ItemsArgs.test_giveup), to exercise the error words.
+uint32_t take_test_giveup() {
+#ifdef RPCCRC_TEST_HOOKS
+  static std::atomic<long> left{[] {
     const char *e = getenv("RPCCRC_TEST_STEAL_GIVEUP");
-    return (e && e[0] == '1') ? 1u : 0u;
-  }();
-  return v;
+    return e ? atol(e) : 0L;
+  }()};
+  return left.fetch_sub(1) > 0 ? 1u : 0u;
+#else
+  return 0u;
+#endif
 }
 
 int max_blocks_for(const DeviceCtx &c) {
@@ -486,7 +508,6 @@ ItemsArgs items_args(const DeviceCtx &c, const uint8_t *base, const uint64_t *of
   a.out = out;
   a.gshift = kRowsGroupShift;
   a.err = c.err;
-  a.test_giveup = test_giveup();
   return a;
 }
 
@@ -542,13 +563,17 @@ bool ragged_steal() {
   return v;
 }
 
+// err: the error word of the call's launches (nullptr: the device's, for the
+// asynchronous entry points; the synchronous ones pass a word of their own).
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s) {
+          uint64_t stride, uint32_t len, uint32_t mode, uint32_t *out, int QB, hipStream_t s, uint32_t *err = nullptr) {
   ItemsArgs a = items_args(c, base, offsets, lengths, n, stride, len, mode, out);
+  if (err) a.err = err;
   StealLease sl;
   if (offsets == nullptr && len <= 4096)
     if (const int rc = sl.get(c, n, QB, s)) return rc;
   a.steal = sl.p;
+  if (a.steal) a.test_giveup = take_test_giveup();
   return map_hip(launch_rows(a, QB, nontemporal(), max_blocks_for(c), s, sl.done_event(), &sl.recorded));
 }
 
@@ -562,7 +587,7 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
 //    (classify before, chunks + fold after) so a long body
 //    does not stream through a single wave.  Not with the packed kernel.
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-           uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route) {
+           uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route, uint32_t *err = nullptr) {
   const int path = g_ragged_path.load(std::memory_order_relaxed);
   const bool nt = nontemporal();
   const int mb = max_blocks_for(c);
@@ -576,6 +601,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   const bool split = !packed && n <= kMaxLaunchItems && (path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
   route = route && !packed && mode == kModeFinal && n <= kMaxLaunchItems;
   ItemsArgs a = items_args(c, base, offsets, lengths, n, 0, 0, mode, out);
+  if (err) a.err = err;
   if (packed) {
     const uint64_t ms = std::min<uint64_t>(kPackedMaxSlices, std::max<uint64_t>(8192, 4 * n));
     size_t bytes = 0;
@@ -701,7 +727,7 @@ __global__ void expand_chunks_inline_kernel(InlineBodies bodies, uint64_t nb, ui
 // blocks that XOR into the zeroed output.  The workspace comes from the
 // device's pool (stream-ordered reuse, no free on this path).
 int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_offsets, const uint64_t *h_lengths,
-                 uint64_t n, uint32_t *d_out, uint64_t chunk, hipStream_t s) {
+                 uint64_t n, uint32_t *d_out, uint64_t chunk, hipStream_t s, uint32_t *err = nullptr) {
   if (chunk % 16 != 0 || chunk > (1ull << 31)) return RPCCRC_EINVAL;
   if (n == 0) return RPCCRC_OK;
   const bool inl = n <= kInlineBodies;
@@ -774,10 +800,12 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   uint64_t *d_lens = nullptr, *d_firsts = nullptr;
   if (fast) {
     ItemsArgs k = items_args(c, d_base + h_offsets[0], nullptr, nullptr, total, chunk, (uint32_t)chunk, kModeRaw, d_raw);
+    if (err) k.err = err;
     StealLease sl; // one-row chunks deal like the north star (items())
     if (chunk <= 4096)
       if (const int rc = sl.get(c, total, 1, s)) return rc;
     k.steal = sl.p;
+    if (k.steal) k.test_giveup = take_test_giveup();
     if (contig) {
       k.zero_out = d_out;
       k.zero_n = (uint32_t)n;
@@ -800,8 +828,9 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
       hipLaunchKernelGGL(expand_chunks_kernel, eg, dim3(256), 0, s, d_bodies, n, chunk, total, d_ioff, d_ilen, d_lens,
                          d_firsts, d_out);
     RPCCRC_TRY(hipGetLastError());
-    RPCCRC_TRY(launch_rows(items_args(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw), 1, nontemporal(),
-                           max_blocks_for(c), s));
+    ItemsArgs k = items_args(c, d_base, d_ioff, d_ilen, total, 0, 0, kModeRaw, d_raw);
+    if (err) k.err = err;
+    RPCCRC_TRY(launch_rows(k, 1, nontemporal(), max_blocks_for(c), s));
   }
   CombineArgs ca;
   ca.raw = d_raw;
@@ -844,6 +873,8 @@ int scalar_ctx_init(ScalarCtx &t) {
   // Coherent: the host polls this word while the kernel may still be running.
   RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.pres), 64, hipHostMallocCoherent));
   *reinterpret_cast<volatile uint64_t *>(t.pres) = 0;
+  t.perr = reinterpret_cast<uint32_t *>(t.pres + 1);
+  *reinterpret_cast<volatile uint32_t *>(t.perr) = 0;
   RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.pin), kScalarZeroCopyMax, hipHostMallocDefault));
   return RPCCRC_OK;
 }
@@ -904,7 +935,7 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
   }
   if (len <= kScalarZeroCopyMax) {
     memcpy(t->pin, src, len);
-    rc = items(*c, t->pin, nullptr, nullptr, 1, 0, len, kModeFinal, t->pout, 1, t->stream);
+    rc = items(*c, t->pin, nullptr, nullptr, 1, 0, len, kModeFinal, t->pout, 1, t->stream, t->perr);
     if (rc) die("kernel launch", rc);
   } else {
     // Device staging borrowed from the device's workspace pool (stream-ordered
@@ -921,15 +952,15 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
     if (hipMemcpyAsync(dbuf, src, len, hipMemcpyHostToDevice, t->stream) != hipSuccess) die("H2D copy", RPCCRC_EIO);
     if (len >= kScalarChunkedMin) {
       const uint64_t off = 0, l64 = len;
-      rc = device_large(*c, dbuf, &off, &l64, 1, dword, 0, t->stream);
+      rc = device_large(*c, dbuf, &off, &l64, 1, dword, 0, t->stream, t->perr);
     } else {
-      rc = items(*c, dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, dword, 1, t->stream);
+      rc = items(*c, dbuf, nullptr, nullptr, 1, 0, len, kModeFinal, dword, 1, t->stream, t->perr);
     }
     if (rc) die("kernel launch", rc);
     if (hipMemcpyAsync(t->pout, dword, 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess) die("D2H copy", RPCCRC_EIO);
   } // the lease returns the staging block here, after its last use was enqueued
   if (hipStreamSynchronize(t->stream) != hipSuccess) die("stream sync", RPCCRC_EIO);
-  if ((rc = device_error(*c))) die("kernel (device error word)", rc);
+  if ((rc = word_error(t->perr))) die("kernel (call error word)", rc);
   const uint32_t r = *t->pout;
   c->scalar->release(t);
   return r;
@@ -939,6 +970,7 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
 
 int pipe_init(HostPipeline &p) {
   if (p.ok) return RPCCRC_OK;
+  if (!p.perr) RPCCRC_TRY(hipHostMalloc(reinterpret_cast<void **>(&p.perr), 64, hipHostMallocCoherent));
   for (HostSlot &s : p.slot) {
     if (!s.stream) RPCCRC_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     if (!s.dbuf) RPCCRC_TRY(hipMalloc(&s.dbuf, kStageBytes));
@@ -965,6 +997,7 @@ int host_batch_run(const DeviceCtx &c, HostPipeline &p, const uint8_t *base, con
                    const uint32_t *lengths, uint64_t n, uint32_t *out) {
   int rc = pipe_init(p);
   if (rc) return rc;
+  *reinterpret_cast<volatile uint32_t *>(p.perr) = 0; // this call's launches report here
   uint64_t i = 0;
   int which = 0;
   while (i < n) {
@@ -979,7 +1012,7 @@ int host_batch_run(const DeviceCtx &c, HostPipeline &p, const uint8_t *base, con
         if ((rc = tmp.get(c.ws, L, s.stream))) return rc;
         RPCCRC_TRY(hipMemcpyAsync(tmp.ptr(), base + offsets[i], L, hipMemcpyHostToDevice, s.stream));
         const uint64_t zero = 0;
-        if ((rc = device_large(c, tmp.ptr(), &zero, &L, 1, s.dout, 0, s.stream))) return rc;
+        if ((rc = device_large(c, tmp.ptr(), &zero, &L, 1, s.dout, 0, s.stream, p.perr))) return rc;
       }
       RPCCRC_TRY(hipMemcpyAsync(s.hout, s.dout, 4, hipMemcpyDeviceToHost, s.stream));
       s.first = i;
@@ -1011,7 +1044,7 @@ int host_batch_run(const DeviceCtx &c, HostPipeline &p, const uint8_t *base, con
     if (hi > lo) RPCCRC_TRY(hipMemcpyAsync(s.dbuf, base + lo, hi - lo, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.doff, s.hoff, cnt * 8, hipMemcpyHostToDevice, s.stream));
     RPCCRC_TRY(hipMemcpyAsync(s.dlen, s.hlen, cnt * 4, hipMemcpyHostToDevice, s.stream));
-    rc = ragged(c, s.dbuf, s.doff, s.dlen, cnt, kModeFinal, s.dout, s.stream, false, true);
+    rc = ragged(c, s.dbuf, s.doff, s.dlen, cnt, kModeFinal, s.dout, s.stream, false, true, p.perr);
     if (rc) return rc;
     RPCCRC_TRY(hipMemcpyAsync(s.hout, s.dout, cnt * 4, hipMemcpyDeviceToHost, s.stream));
     s.first = i;
@@ -1028,7 +1061,7 @@ int host_batch(DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const
                uint32_t *out) {
   HostPipeline *p = c.pipes->acquire();
   int rc = host_batch_run(c, *p, base, offsets, lengths, n, out);
-  if (rc == RPCCRC_OK) rc = device_error(c); // every launch of this call has completed
+  if (rc == RPCCRC_OK) rc = word_error(p->perr); // every launch of this call has completed
   if (rc) // leave the pipeline idle for its next borrower
     for (HostSlot &s : p->slot)
       if (s.busy) {
@@ -1104,7 +1137,7 @@ int rpc_crc32_device_batch_bounded(const uint8_t *d_base, const uint64_t *d_offs
   if (n == 0) return RPCCRC_OK;
   if (!d_base || !d_offsets || !d_lengths || !d_out) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
-  int rc = get_ctx(&c);
+  int rc = get_async_ctx(&c);
   if (rc) return rc;
   // A bound below the route threshold: no body can take the big-body route, so
   // its passes (classify before the rows pass; plan, expand, chunk rows and
@@ -1120,7 +1153,7 @@ int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_le
   if (n == 0) return RPCCRC_OK;
   if (!d_base || !d_out) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
-  int rc = get_ctx(&c);
+  int rc = get_async_ctx(&c);
   if (rc) return rc;
   // Four bodies per 4 KiB row when every body plus its pad to a 16-byte end
   // fits a 1 KiB quarter (QB = 4); otherwise one body per row sequence.
@@ -1135,7 +1168,7 @@ int rpc_crc32_device_large(const uint8_t *d_base, const uint64_t *h_offsets, con
   if (n == 0) return RPCCRC_OK;
   if (!d_base || !h_offsets || !h_lengths || !d_out) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
-  int rc = get_ctx(&c);
+  int rc = get_async_ctx(&c);
   if (rc) return rc;
   return device_large(*c, d_base, h_offsets, h_lengths, n, d_out, chunk_bytes, static_cast<hipStream_t>(stream));
 }
@@ -1146,7 +1179,7 @@ int rpc_frames_verify_device(const uint8_t *d_stream, uint64_t stream_bytes, con
   if (n == 0) return RPCCRC_OK;
   if (!d_stream || !d_frame_offsets || !d_verdict || n >= 0xFFFFFFFFull) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
-  int rc = get_ctx(&c);
+  int rc = get_async_ctx(&c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   Lease wsl;
@@ -1171,7 +1204,7 @@ int rpc_frames_stamp_device(uint8_t *d_stream, uint64_t stream_bytes, const uint
   if (n == 0) return RPCCRC_OK;
   if (!d_stream || !d_frame_offsets || !d_body_lens || n >= 0xFFFFFFFFull) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
-  int rc = get_ctx(&c);
+  int rc = get_async_ctx(&c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   Lease wsl;
@@ -1197,12 +1230,24 @@ int rpc_crc32_fill_random_device(void *d_dst, uint64_t nbytes, uint64_t seed, vo
 }
 
 int rpc_crc32_stream_read_device(const void *d_src, uint64_t nbytes, int pattern, int nontemporal, void *stream) {
-  if (!d_src || nbytes % 4096 != 0 || (pattern != 0 && pattern != 1)) return RPCCRC_EINVAL;
+  if (!d_src || nbytes % 4096 != 0 || pattern < 0 || pattern > 2) return RPCCRC_EINVAL;
   DeviceCtx *c = nullptr;
-  int rc = get_ctx(&c);
+  int rc = get_async_ctx(&c);
   if (rc) return rc;
-  return map_hip(launch_stream_read(d_src, nbytes, pattern, nontemporal != 0, max_blocks_for(*c), nullptr,
-                                    static_cast<hipStream_t>(stream)));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (pattern == 2) { // the rows kernel's dealing and load shape (launch_stream_rows)
+    const uint64_t n = nbytes / 4096;
+    StealLease sl;
+    if ((rc = sl.get(*c, n, 1, s))) return rc;
+    if (!sl.p) return RPCCRC_EINVAL; // too small to deal dynamically
+    Lease sink;
+    if ((rc = sink.get(c->ws, 16 * 4 * (size_t)max_blocks_for(*c), s))) return rc;
+    ItemsArgs a = items_args(*c, static_cast<const uint8_t *>(d_src), nullptr, nullptr, n, 4096, 4096, kModeFinal,
+                             reinterpret_cast<uint32_t *>(sink.ptr()));
+    a.steal = sl.p;
+    return map_hip(launch_stream_rows(a, max_blocks_for(*c), s, sl.done_event(), &sl.recorded));
+  }
+  return map_hip(launch_stream_read(d_src, nbytes, pattern, nontemporal != 0, max_blocks_for(*c), nullptr, s));
 }
 
 int rpc_crc32_set_options(int nontemporal, int max_blocks) {
@@ -1222,7 +1267,16 @@ int rpc_crc32_set_ragged_path(int path) {
 
 int rpc_crc32_device_status(void) {
   DeviceCtx *c = nullptr;
-  return get_ctx(&c);
+  return get_async_ctx(&c);
+}
+
+int rpc_crc32_device_clear_status(void) {
+  DeviceCtx *c = nullptr;
+  const int rc = get_ctx(&c);
+  if (rc) return rc;
+  const int was = device_error(*c);
+  *reinterpret_cast<volatile uint32_t *>(c->err) = 0u;
+  return was;
 }
 
 const char *rpc_crc32_strerror(int err) {

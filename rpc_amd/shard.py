@@ -40,6 +40,14 @@ def max_over_ranks(dist, value: float, device=None) -> float:
     return float(t.item())
 
 
+def min_over_ranks(dist, value: float, device=None) -> float:
+    import torch
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def sum_over_ranks(dist, value: int, device=None) -> int:
     import torch
 

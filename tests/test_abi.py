@@ -98,3 +98,15 @@ def test_null_and_empty_need_no_device():
     assert _lib.rpc_crc32(None, 5) == 0
     assert _lib.rpc_crc32(b"abc", 0) == 0
     assert _lib.rpc_crc32(b"abc", 2**32) == 0  # len mod 2^32 == 0
+
+
+def test_test_library_exports_the_same_abi():
+    """librpccrc_test.so (fault-injection build for the error-word tests) exports the
+    same symbols; only it knows the test switch (the product library must
+    not read RPCCRC_TEST_STEAL_GIVEUP)."""
+    test_lib = os.path.join(REPO, "rpc_amd", "lib", "librpccrc_test.so")
+    assert os.path.exists(test_lib), "run __graft_entry__.build()"
+    out = subprocess.run(["nm", "-D", "--defined-only", test_lib], capture_output=True, text=True, check=True).stdout
+    assert sorted(line.split()[-1] for line in out.splitlines() if line.strip()) == header_symbols()
+    assert b"RPCCRC_TEST_STEAL_GIVEUP" in open(test_lib, "rb").read()
+    assert b"RPCCRC_TEST_STEAL_GIVEUP" not in open(LIB, "rb").read()

@@ -41,3 +41,26 @@ def test_gpus1_runs_in_process():
     rc, lines, err = _launch(1)
     assert rc == 0, err[-3000:]
     assert lines == [{"rank": 0, "world": 1, "local_rank": 0, "gpus": 1, "master": None, "config": "ns"}]
+
+
+def test_gpus2_reductions_report_slowest_rank():
+    """at N > 1 the roofline is the SLOWEST rank's (as `value` is) and
+    the line carries the per-rank spread.  Two gloo ranks on the CPU with synthetic
+    launch times (rank r: (1 + r / 10) ms) through bench.py's own reduction and
+    roofline code (RPCCRC_BENCH_REDUCE_ONLY)."""
+    env = dict(os.environ, RPCCRC_BENCH_REDUCE_ONLY="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    r = lines[0]["roofline"]
+    assert r["per_rank"]["ranks"] == 2
+    assert r["per_rank"]["min_us"] == 1000.0 and r["per_rank"]["max_us"] == 1100.0
+    assert r["avg_launch_us"] == 1100.0
+    algo = (1 << 23) * (4096 + 4)  # C3, the N > 1 default: 8M x 4 KiB per rank
+    assert r["algo_bytes_per_launch"] == algo
+    assert abs(r["achieved"] - algo / 1.1e-3 / 1e9) < 0.1
+    # value: both ranks' bytes over the slowest rank's wall time
+    assert abs(lines[0]["value"] - 2 * (1 << 23) * 4096 / 1.1e-3 / (1 << 30)) < 0.1

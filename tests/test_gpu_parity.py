@@ -109,22 +109,40 @@ def test_drop_in_staging_pool_with_concurrent_batch():
     assert rpc_amd.device_status() == 0
 
 
-def test_device_error_word_reports_steal_giveup():
-    """a wave that gives up a bounded wait of the tail-stealing
-    protocol stores into the device error word, and the host reports RPCCRC_EIO
-    (sticky) instead of returning stale CRCs with rc 0.  Forced in a child process
-    with the test-only RPCCRC_TEST_STEAL_GIVEUP=1 (every pool round gives up)."""
+def test_error_words_per_call_and_clearable():
+    """VERDICT r03 #8 / ADVICE r03: a wave that gives up a bounded wait of the
+    tail-stealing protocol stores into the error word of ITS call, and the host
+    reports RPCCRC_EIO instead of returning stale CRCs with rc 0.
+      * synchronous calls (host batch, drop-in) own a word per call: the failing
+        call returns -5, the device word stays clear, the next call works;
+      * asynchronous calls report through the device word: -5 from
+        rpc_crc32_device_status and from every later asynchronous call, until
+        rpc_crc32_device_clear_status; synchronous calls keep working meanwhile.
+    Forced in a child process on the fault-injection build librpccrc_test.so
+    (RPCCRC_TEST_STEAL_GIVEUP=2: the next two stealing launches give up)."""
     import os
     import subprocess
     import sys
     code = r"""
 import numpy as np, torch, rpc_amd
+from oracle import oracle
 torch.cuda.set_device(0)
+assert rpc_amd.device_status() == 0
+# (a) host batch, one 512 MiB body (> one 256 MiB stage: chunked, stealing) -> give-up #1
+big = oracle.splitmix_bytes(512 << 20, 0xB16E)
+want_big = oracle.crc32(big)
+offs, lens = np.array([0], np.uint64), np.array([512 << 20], np.uint32)
+try:
+    rpc_amd.crc32_batch(big, offs, lens)
+    print("host1", 0)
+except rpc_amd.RpcCrcError as e:
+    print("host1", e.code)
+print("status_after_host", rpc_amd.device_status())
+# (b) asynchronous device batch -> give-up #2, recorded in the device word
 n, L = 65536, 4096
 base = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
 rpc_amd.fill_random(base, 0x6E7)
-assert rpc_amd.device_status() == 0
-rpc_amd.device_uniform(base, n, L)     # deals its last rounds from the steal pool
+rpc_amd.device_uniform(base, n, L)
 torch.cuda.synchronize()
 print("status", rpc_amd.device_status())
 try:
@@ -132,12 +150,23 @@ try:
     print("next", 0)
 except rpc_amd.RpcCrcError as e:
     print("next", e.code)
+# (c) synchronous calls are not affected by the device word
+print("dropin", rpc_amd.rpc_crc32(b"123456789") == 0xCBF43926)
+print("host2", int(rpc_amd.crc32_batch(big, offs, lens)[0]) == want_big)
+# (d) clear: asynchronous calls work again, every CRC exact
+print("clear", rpc_amd.device_clear_status(), rpc_amd.device_status())
+got = rpc_amd.device_uniform(base, n, L).cpu().numpy().view(np.uint32)
+print("after_clear", bool(np.array_equal(got, oracle.crc32_uniform(base.cpu().numpy(), n, L))))
 """
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, RPCCRC_TEST_STEAL_GIVEUP="1", PYTHONPATH=repo)
+    env = dict(os.environ, RPCCRC_TEST_STEAL_GIVEUP="2", PYTHONPATH=repo,
+               RPCCRC_LIB=os.path.join(repo, "rpc_amd", "lib", "librpccrc_test.so"))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env, cwd=repo)
     assert p.returncode == 0, p.stderr[-3000:]
-    assert "status -5" in p.stdout and "next -5" in p.stdout, p.stdout
+    out = p.stdout
+    for want in ("host1 -5", "status_after_host 0", "status -5", "next -5", "dropin True", "host2 True",
+                 "clear -5 0", "after_clear True"):
+        assert want in out, (want, out)
 
 
 def test_drop_in_frames(golden):
@@ -563,6 +592,70 @@ def test_c2_ragged_loguniform_sample():
         finally:
             rpc_amd.set_ragged_path("auto")
         assert np.array_equal(got, other), path
+
+
+def _check_ragged_slices(base, offs, lens, got, slice_bytes=4 << 30):
+    """Every CRC of a contiguous ragged batch against the threaded oracle, copying
+    the device bytes back ~slice_bytes at a time."""
+    ends = np.cumsum(lens, dtype=np.uint64)
+    lo = 0
+    n = lens.size
+    while lo < n:
+        hi = int(np.searchsorted(ends, np.uint64(int(offs[lo]) + slice_bytes), side="right"))
+        hi = max(hi, lo + 1)
+        b0, b1 = int(offs[lo]), int(offs[hi - 1]) + int(lens[hi - 1])
+        part = base[b0:b1].cpu().numpy()
+        want = oracle.crc32_batch_mt(part, offs[lo:hi] - np.uint64(b0), lens[lo:hi])
+        bad = np.flatnonzero(got[lo:hi] != want)
+        assert bad.size == 0, f"{bad.size} mismatches, first body {lo + int(bad[0])}, rounds " \
+                              f"{sorted(set(((lo + bad) // 32).tolist()))[:8]}"
+        del part
+        lo = hi
+
+
+def test_c2_full_size_every_crc():
+    """config C2 at its BASELINE size -- 4M bodies, log-uniform
+    64 B - 64 KiB (seed 0x5EED0004), ~37 GiB back to back, exactly the bench's
+    workload (bench.py Workload "c2": the bounded call with max_len = 64 KiB) --
+    EVERY CRC against the oracle (reference crc.c:4-9 body by body), in ~4 GiB
+    slices.  The ragged DYN launch deals 8x the rounds of the 1/8 sample; a lost
+    or duplicated round is 32 bodies, which a sample misses.  The unbounded call
+    (route classify + empty route passes) must give the same outputs."""
+    n = 1 << 22
+    lens = oracle.loguniform_lengths(n, 0x5EED0004)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+    base = torch.empty((total + 15) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0x5EED0004)
+    doffs, dlens = to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))
+    got = u32(rpc_amd.device_batch(base, doffs, dlens, max_len=int(lens.max())))
+    plain = u32(rpc_amd.device_batch(base, doffs, dlens))
+    assert np.array_equal(got, plain)
+    _check_ragged_slices(base, offs, lens, got)
+    assert rpc_amd.device_status() == 0
+
+
+def test_dyn_ragged_batch_with_huge_unrouted_body():
+    """a DYN-sized ragged batch whose length bound (64 KiB)
+    keeps a 512 MiB body off the big-body route, so ONE wave walks it (~0.1-0.3 s)
+    while its siblings run 8 rounds ahead and wait for its output-ring slot.  The
+    wait must outlast it (round 3's 0.1 s spin cap reported a false EIO and lost
+    the round): every CRC exact, device status clean."""
+    n_small = 200000
+    rng = np.random.default_rng(0xB16)
+    lens = rng.integers(1, 4000, n_small).astype(np.uint32)
+    big = 512 << 20
+    pos = 1000  # early in the batch: its round is dealt first, the rest run past it
+    lens = np.insert(lens, pos, np.uint32(big))
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+    base = torch.empty((total + 15) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0xB16B0D7)
+    got = u32(rpc_amd.device_batch(base, to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32)),
+                                   max_len=64 << 10))
+    torch.cuda.synchronize()
+    assert rpc_amd.device_status() == 0
+    _check_ragged_slices(base, offs, lens, got, slice_bytes=1 << 30)
 
 
 def test_c4_large_bodies():
