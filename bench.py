@@ -328,21 +328,26 @@ def rx_ring_probe():
 
 
 def scalar_latency_probe():
-    """Per-call latency of the drop-in rpc_crc32 (one GPU kernel per call) at 12 B,
-    68 B and 1 KiB on 1 and 10 threads, beside the reference crc.c on the same host
-    (tools/scalar_bench.c; VERDICT r01 'scalar path: measure it')."""
+    """Per-call latency of the drop-in rpc_crc32 at 12 B, 68 B and 1 KiB on 1 and 10
+    threads, beside the reference crc.c on the same host (tools/scalar_bench.c):
+    through the resident drop-in service (the default) and, for
+    comparison, with a kernel launch per call (RPCCRC_SERVICE=0)."""
     import subprocess
     exe = os.path.join(REPO, "tools", "scalar_bench")
     if not os.path.exists(exe):
         return None
     ref = os.path.join(REPO, "oracle", "_ref", "libref_crc.so")
-    p = subprocess.run([exe] + ([ref] if os.path.exists(ref) else []), capture_output=True, text=True, timeout=300)
-    try:
-        r = json.loads(p.stdout.strip().splitlines()[-1])
-    except (ValueError, IndexError):
-        return {"error": (p.stderr or p.stdout)[-300:], "rc": p.returncode}
-    r["rc"] = p.returncode
-    return r
+    out = {}
+    for name, env in (("service", {}), ("launch_per_call", {"RPCCRC_SERVICE": "0"})):
+        p = subprocess.run([exe] + ([ref] if os.path.exists(ref) else []), capture_output=True, text=True,
+                           timeout=300, env=dict(os.environ, **env))
+        try:
+            r = json.loads(p.stdout.strip().splitlines()[-1])
+        except (ValueError, IndexError):
+            r = {"error": (p.stderr or p.stdout)[-300:]}
+        r["rc"] = p.returncode
+        out[name] = r
+    return out
 
 
 def frames_lifted_probe(device, n=1024, reps=5, seed=0x5EED0007):

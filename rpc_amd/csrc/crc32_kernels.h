@@ -121,6 +121,28 @@ uint32_t scalar_seg_log2(uint32_t len);
 hipError_t launch_scalar(const uint8_t *stage, uint32_t len, const uint4 *tab, const uint32_t *tq, uint64_t *result,
                          uint32_t seq, hipStream_t stream);
 
+// ---- drop-in service (crc32_service.hip) ---------------------
+// A resident one-workgroup kernel answers drop-in calls of <= kSvcMaxLen bytes
+// through request slots in pinned, coherent host memory: no launch per call.
+constexpr uint32_t kSvcWaves = 4;                      // waves of the service workgroup
+constexpr uint32_t kSvcPer = 4;                        // slots per wave
+constexpr uint32_t kSvcSlots = kSvcWaves * kSvcPer;    // concurrent drop-in calls served
+constexpr uint32_t kSvcMaxLen = 1024;                  // MAX_BODY_LEN (rpc.h:17)
+constexpr uint32_t kSvcStop = 0, kSvcExited = 1;       // SvcShared::ctl words
+struct SvcShared {
+  uint32_t seq[kSvcSlots];            // host: request sequence of each slot (written last)
+  uint32_t len[kSvcSlots];            // host: body length
+  uint64_t res[kSvcSlots][8];         // device: {crc, seq} (crc in the low half), one 64-B line per slot
+  uint32_t ctl[16];                   // [kSvcStop] host: leave now; [kSvcExited] device: last instance that left
+  uint8_t body[kSvcSlots][kSvcMaxLen]; // host: the body, right-aligned in 64 * seg bytes (seg 4 / 8 / 16)
+};
+// kshift: 3 x 64 words, kshift[c][L] = x^(8 * seg_c * (63 - L)) mod P for seg 4, 8, 16.
+// The kernel leaves after idle_ticks (s_memrealtime, 100 MHz) without a
+// request or after life_ticks in all; it then stores `instance` into
+// ctl[kSvcExited].
+hipError_t launch_service(SvcShared *sh, const uint32_t *tq, const uint32_t *kshift, uint64_t idle_ticks,
+                          uint64_t life_ticks, uint32_t instance, hipStream_t stream);
+
 // A large body of rpc_crc32_device_large: bytes [off, off + len) of the base
 // buffer, its end-aligned chunks at raw[chunk_first ...].
 struct LargeBody {

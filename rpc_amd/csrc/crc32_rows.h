@@ -580,6 +580,25 @@ constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
 #define RPCCRC_STEAL_AHEAD 1
 #endif
 constexpr uint32_t kStealAhead = RPCCRC_STEAL_AHEAD;
+// Pool UNITS per dealing round (1, 2 or 4): the pool is claimed in units of
+// kRound / kStealSplit tasks, kStealSplit * kStealAhead units ahead (the same
+// lead time).  When the pool runs dry a workgroup still holds at most its
+// current unit plus the claimed-ahead ones, so smaller units shorten the
+// launch's drain (C1: ~12 us of exit spread with whole-round claims,
+// profiles/r03h/timeline_steal_c1.log).  A static round still completes as one
+// unit; a pool round completes per unit (its own done count and store), and
+// its ring slot is freed when all of its units are stored.
+#ifndef RPCCRC_STEAL_SPLIT
+#define RPCCRC_STEAL_SPLIT 1
+#endif
+constexpr uint32_t kStealSplit = RPCCRC_STEAL_SPLIT;
+static_assert(kStealSplit == 1 || kStealSplit == 2 || kStealSplit == 4, "pool units per round: 1, 2 or 4");
+#ifndef RPCCRC_STEAL_AHEAD_UNITS
+#define RPCCRC_STEAL_AHEAD_UNITS (RPCCRC_STEAL_AHEAD * RPCCRC_STEAL_SPLIT)
+#endif
+constexpr uint32_t kStealAheadUnits = RPCCRC_STEAL_AHEAD_UNITS;
+static_assert(kStealAheadUnits >= 1 && kStealAheadUnits <= kStealAhead * kStealSplit,
+              "claims at most kStealAhead rounds ahead (the host sizes steal_s >= kStealAhead)");
 constexpr uint32_t kStealQ = 16;                      // LDS queue ring
 constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
 // Bounded waits.  Both waits end by protocol (a claim is published by the wave
@@ -602,7 +621,14 @@ __device__ __forceinline__ bool wait_expired(uint32_t spin, uint64_t &t0) {
   if (spin == 0) t0 = now;
   return now - t0 > kWaitCapTicks;
 }
-constexpr uint32_t dyn_ring_words(int QB) { return 1 + 2 * dyn_slots(QB) + dyn_slots(QB) * dyn_round(QB) * (uint32_t)QB; }
+// DYN control block: [0] task counter, kDynSlots * kStealSplit unit done
+// counts, kDynSlots slot generations, kDynSlots stored-unit counts (split pool
+// rounds only), then the CRC ring (QB CRCs per task, kRound tasks per slot).
+constexpr uint32_t dyn_done_words(int QB) { return dyn_slots(QB) * kStealSplit; }
+constexpr uint32_t dyn_gen_ofs(int QB) { return 1 + dyn_done_words(QB); }
+constexpr uint32_t dyn_stored_ofs(int QB) { return dyn_gen_ofs(QB) + dyn_slots(QB); }
+constexpr uint32_t dyn_ringbuf_ofs(int QB) { return dyn_stored_ofs(QB) + (kStealSplit > 1 ? dyn_slots(QB) : 0u); }
+constexpr uint32_t dyn_ring_words(int QB) { return dyn_ringbuf_ofs(QB) + dyn_slots(QB) * dyn_round(QB) * (uint32_t)QB; }
 constexpr uint32_t dyn_ctl_words(int QB) { return dyn_ring_words(QB) + kStealCtlWords; }
 
 template <int QB, bool NT, bool RAGGED = false, int ABL = 0, int DEPTH = 1, bool DYN = false, bool STEAL = false>
@@ -612,13 +638,15 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   static_assert(!STEAL || DYN, "stealing: DYN launches");
   constexpr uint32_t kRound = dyn_round(QB); // tasks per dealing round
   constexpr uint32_t kDynSlots = dyn_slots(QB);
+  constexpr uint32_t kUnit = kRound / kStealSplit; // tasks per pool unit (tail stealing)
+  constexpr uint32_t kGen = dyn_gen_ofs(QB), kStored = dyn_stored_ofs(QB), kRingBuf = dyn_ringbuf_ofs(QB);
   // sub-row first rows: ragged QB = 1 with the plain chain (image V3 adds SQ)
   constexpr bool kSub = kSubRows && QB == 1 && RAGGED && !kTwoChains &&
                         (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblHalfChain | kRowsAblNoSub)) == 0;
   constexpr uint32_t kImgBytes = kSub ? kLdsBytesV3 : kLdsBytesV2;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kImgBytes / 4];
-  // DYN control block: [0] task counter, [1..S] done counts, [1+S..2S] slot
-  // rounds (generation), then the CRC ring (QB CRCs per task).
+  // DYN control block (dyn_ring_words): task counter, unit done counts, slot
+  // generations (slot s starts at round s), stored-unit counts, CRC ring.
   __shared__ uint32_t s_ctl[DYN ? (STEAL ? dyn_ctl_words(QB) : dyn_ring_words(QB)) : 1];
   // kEarlyRow: each wave's first task is static (DYN: counter index = wave, so
   // the LDS counter starts at 16), and its first row's loads are issued between
@@ -626,9 +654,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // overlaps the image copy instead of following the barrier.
   constexpr bool kEarly = kEarlyRow && (ABL & kRowsAblTimes) == 0;
   if constexpr (DYN) {
-    if (threadIdx.x <= 2 * kDynSlots)
-      s_ctl[threadIdx.x] = (threadIdx.x > kDynSlots) ? threadIdx.x - 1 - kDynSlots
-                                                      : ((threadIdx.x == 0u && kEarly) ? 16u : 0u);
+    if (threadIdx.x < kRingBuf)
+      s_ctl[threadIdx.x] = (threadIdx.x >= kGen && threadIdx.x < kStored) ? threadIdx.x - kGen
+                                                                          : ((threadIdx.x == 0u && kEarly) ? 16u : 0u);
     if (STEAL && threadIdx.x < 3 + kStealQ) s_ctl[dyn_ring_words(QB) + threadIdx.x] = 0u; // tail/done/inflight/tags
   }
   // Device-side item counts (split lists, big-body chunks) may be 0: leave
@@ -753,7 +781,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   }();
   const bool steal = STEAL && steal_s != 0u;
   const uint32_t pool_first = steal_s * nblk; // first pool (global) round
-  const uint32_t pool_n = steal ? (n_tasks + kRound - 1) / kRound - pool_first : 0u;
+  const uint32_t pool_n = steal ? (n_tasks + kUnit - 1) / kUnit - pool_first * kStealSplit : 0u; // pool units
   uint32_t *q_ctl = s_ctl + (STEAL ? dyn_ring_words(QB) : 0u);
   uint32_t *q_tail = q_ctl, *q_done = q_ctl + 1, *q_inflight = q_ctl + 2;
   uint32_t *q_tag = q_ctl + 3, *q_id = q_ctl + 3 + kStealQ;
@@ -794,10 +822,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     }
     has_claim = false;
   };
-  // The wave taking local round r's first task claims a pool round for the
-  // workgroup (for use kStealAhead rounds later).
+  // The wave taking a local unit's first task claims a pool unit for the
+  // workgroup (for use kStealAheadUnits units later).
   auto claim_if_first = [&](uint32_t c) { // uniform
-    if (!steal || c % kRound != 0u || c / kRound + kStealAhead < steal_s) return;
+    if (!steal || c % kUnit != 0u || c / kUnit + kStealAheadUnits < steal_s * kStealSplit) return;
     publish(); // at most one claim in flight per wave
     uint32_t go = 0;
     if (lane == 0 && lds_ld_acq(q_done) == 0u) {
@@ -817,7 +845,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     const uint32_t r = c / kRound;
     more = true;
     if (!steal || r < steal_s) return dyn_task(c);
-    const uint32_t q = r - steal_s, k = q % kStealQ;
+    const uint32_t q = c / kUnit - steal_s * kStealSplit, k = q % kStealQ; // the workgroup's q-th pool unit
     if (a.test_giveup != 0u) { // test-only: take the give-up path below deterministically
       if (lane == 0) report_err(kErrStealWait);
       more = false;
@@ -835,7 +863,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (st == 1u) id = q_id[k];
       }
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
-      if (st == 1u) return ((pool_first + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kRound) | (c % kRound);
+      if (st == 1u)
+        return ((pool_first * kStealSplit + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kUnit) | (c % kUnit);
       if (st == 2u) break;
       if (wait_expired(spin, t0)) { // never in a healthy launch: fail loudly, do not hang
         if (lane == 0) report_err(kErrStealWait);
@@ -1012,31 +1041,41 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     // DYN output: CRC of the task with counter index c into the LDS ring; the
     // wave completing a round stores the round's CRCs as one whole line.
+    // A pool round completes per unit (kUnit tasks: its own done count and
+    // store); its slot is freed once all kStealSplit units are stored.
     auto dyn_out = [&](uint32_t c, uint32_t tsk, uint32_t res) {
       const uint32_t rnd = c / kRound, idx = c % kRound, slot = rnd % kDynSlots;
-      uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots;
+      const bool split = kStealSplit > 1 && steal && rnd >= steal_s; // a pool round: per-unit completion
+      const uint32_t usz = split ? kUnit : kRound, unit = split ? idx / kUnit : 0u;
+      uint32_t *done = s_ctl + 1 + slot * kStealSplit + unit, *gen = s_ctl + kGen, *ring = s_ctl + kRingBuf;
       uint32_t old = 0;
       publish(); // the ring wait below must not hold a claim
       if (lane == 0) {
         // the slot still holds an older round that a slow wave has not finished
         ring_wait(gen, slot, rnd);
         ring[slot * kRound + idx] = res;
-        old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      // the round's first global task (static rounds: from the local round)
-      const uint32_t base = steal ? tsk & ~(kRound - 1u) : (rnd * nblk + vb) * kRound;
-      const uint32_t cnt = (n_tasks - base < kRound) ? n_tasks - base : kRound;
-      if (old + 1u == cnt) { // this wave completed the round
-        const uint32_t v = ring[slot * kRound + (lane % kRound)];
+      // the unit's first global task (whole rounds and pool units are aligned)
+      const uint32_t base = tsk & ~(usz - 1u);
+      const uint32_t cnt = (n_tasks - base < usz) ? n_tasks - base : usz;
+      if (old + 1u == cnt) { // this wave completed the unit
+        const uint32_t v = ring[slot * kRound + unit * kUnit + (lane % usz)];
         if constexpr ((ABL & kRowsAblNoStore) == 0) {
           if (lane < cnt) store_out(a.out + oidx(base + lane), v);
         } else {
           sink ^= v;
         }
         if (lane == 0) {
-          done[slot] = 0;
-          __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          *done = 0;
+          bool last = true;
+          if (split) {
+            uint32_t *stored = s_ctl + kStored + slot;
+            last = __hip_atomic_fetch_add(stored, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1u == kStealSplit;
+            if (last) *stored = 0;
+          }
+          if (last) __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         j0 += cnt;
       }
@@ -1573,31 +1612,41 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     auto dyn_out4 = [&](uint32_t c, uint32_t tsk, const uint32_t (&v)[4]) {
       constexpr uint32_t kW = kRound * 4; // CRCs per round (64 or 128)
       const uint32_t rnd = (uint32_t)(c / kRound), idx = (uint32_t)(c % kRound), slot = rnd % kDynSlots;
-      uint32_t *done = s_ctl + 1, *gen = s_ctl + 1 + kDynSlots, *ring = s_ctl + 1 + 2 * kDynSlots + slot * kW;
+      const bool split = kStealSplit > 1 && steal && rnd >= steal_s; // a pool round: per-unit completion (QB = 1)
+      const uint32_t usz = split ? kUnit : kRound, unit = split ? idx / kUnit : 0u;
+      uint32_t *done = s_ctl + 1 + slot * kStealSplit + unit, *gen = s_ctl + kGen;
+      uint32_t *ring = s_ctl + kRingBuf + slot * kW;
       uint32_t old = 0;
       publish(); // the ring wait below must not hold a claim
       if (lane == 0) {
         ring_wait(gen, slot, rnd);
 #pragma unroll
         for (int b = 0; b < 4; ++b) ring[idx * 4 + b] = v[b];
-        old = __hip_atomic_fetch_add(&done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      // first group of the round
-      const uint32_t base = steal ? tsk & ~(kRound - 1u) : (rnd * nblk + vb) * kRound;
-      const uint32_t cnt = (ngroups - base < kRound) ? (uint32_t)(ngroups - base) : kRound;
+      // first group of the unit (whole rounds and pool units are aligned)
+      const uint32_t base = tsk & ~(usz - 1u);
+      const uint32_t cnt = (ngroups - base < usz) ? (uint32_t)(ngroups - base) : usz;
       if (old + 1u == cnt) {
-        const uint32_t ibase = 4 * base;
-        const uint32_t nit = (n - ibase < kW) ? (uint32_t)(n - ibase) : kW;
-        const uint32_t v0 = ring[lane];
+        const uint32_t ibase = 4 * base, w = 4 * usz; // the unit's CRCs: 4 per group
+        const uint32_t nit = (n - ibase < w) ? (uint32_t)(n - ibase) : w;
+        const uint32_t *u = ring + unit * kUnit * 4;
+        const uint32_t v0 = u[lane % w];
         if (lane < nit) store_out(a.out + oidx(ibase + lane), v0);
-        if constexpr (kW > 64) {
-          const uint32_t v1 = ring[64 + lane];
+        if (w > 64) {
+          const uint32_t v1 = u[64 + lane]; // (w = 128)
           if (64 + lane < nit) store_out(a.out + oidx(ibase + 64 + lane), v1);
         }
         if (lane == 0) {
-          done[slot] = 0;
-          __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          *done = 0;
+          bool last = true;
+          if (split) {
+            uint32_t *stored = s_ctl + kStored + slot;
+            last = __hip_atomic_fetch_add(stored, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1u == kStealSplit;
+            if (last) *stored = 0;
+          }
+          if (last) __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         j0 += cnt;
       }

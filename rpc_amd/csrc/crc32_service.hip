@@ -1,0 +1,190 @@
+// rpc_amd/csrc/crc32_service.hip -- the drop-in rpc_crc32 (crc.h:8, crc.c:4-9)
+// without a kernel launch per call: a small resident SERVICE kernel (one
+// workgroup of kSvcWaves waves) polls request slots in pinned host memory and
+// answers each with one wave.
+//
+// Why: a launch + completion costs ~6.6 us of the 8.3 us a one-wave-kernel
+// call took (tools/latency_probe.hip, profiles/r02/r02n_*), against 0.025 us
+// for the reference crc.c on a 68-B body.  The reference's callers make one
+// call per RPC (client stamp rpc_async.c:525, recv verify :219; server verify
+// rpc_server_main.c:227, stamp :249), from up to 10 threads.
+//
+// Protocol (SvcShared, hipHostMallocCoherent: every access below bypasses the
+// GPU caches -- sc0 sc1 loads / stores, no cache-wide fence):
+//   host   writes the body right-aligned into body[slot] (virtual buffer of
+//          64 * seg bytes, seg = 4 / 8 / 16 bytes per lane by length), then
+//          len[slot], then bumps seq[slot] (x86 stores stay in order);
+//   wave   polls the seq words of its kSvcPer slots (one load from one line,
+//          lane i = slot i); a seq it has not answered is a request: it reads len and the
+//          body (every lane its seg bytes), computes the CRC and stores
+//          {crc, seq} into res[slot] (one 64-bit store);
+//   host   spins on res[slot] until the seq matches.
+// The waves share the time of the last request in LDS (4 bytes) and all leave
+// after idle_ticks without one, after the kernel's lifetime cap, or when the
+// host sets ctl[kSvcStop]; the last wave out stores its instance number into
+// ctl[kSvcExited], so the host knows when to launch a new instance (a request
+// that arrives while an instance is leaving is picked up by the next one:
+// pending = seq not yet answered in res).
+//
+// Resources: NO table image in LDS and few registers, so the kernel can sit
+// on a CU next to a rows-kernel workgroup (155 KiB LDS each, one per CU, a
+// persistent grid over all CUs): the CRC is bit-serial --
+//   chain: crc0 of each 32-bit word by the bit loop (3 VALU per bit);
+//   merge: lane L's segment crc0 times x^(8 * seg * (63 - L)) mod P (per-lane
+//          constant from the host, kSvcShift), bit-serial, then an XOR over
+//          the 64 lanes;
+//   final: ~(Tq[len] ^ crc0), Tq[len] = A_len(0xFFFFFFFF) (zlib's conditioning).
+#include <hip/hip_runtime.h>
+
+#include "crc32_gf2.h"
+#include "crc32_kernels.h"
+#include "crc32_layout.h"
+
+namespace rpccrc {
+
+namespace {
+
+// crc0 of one 32-bit word x (state already XORed in): the bit loop
+// x = x * x (mod P) 32 times, 3 VALU per bit and one constant (a table of the
+// 32 single-bit results takes 2 VALU per bit but keeps 32 constants live).
+__device__ __forceinline__ uint32_t crc0_word(uint32_t x) {
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)x, 0, 1); // all ones iff bit 0
+    x = __builtin_amdgcn_bitop3_b32(x >> 1, lo, kPoly, 0x6A);         // (x >> 1) ^ (lo & P)
+  }
+  return x;
+}
+
+// a * b mod P, bit-serial over a (reflected: bit 31 = x^0).  `a` is shifted
+// along rather than tested bit by bit: independent bit tests were all hoisted
+// (one live VGPR each).
+__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  // b's powers b * x^i do not depend on a: without this barrier they were
+  // precomputed outside the poll loop, 32 live VGPRs per size class
+  __asm__ volatile("" : "+v"(b));
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t m = (uint32_t)((int32_t)a >> 31);
+    a <<= 1;
+    p = __builtin_amdgcn_bitop3_b32(p, m, b, 0x6A); // p ^ (m & b)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
+    b = __builtin_amdgcn_bitop3_b32(b >> 1, lo, kPoly, 0x6A); // b * x
+  }
+  return p;
+}
+
+// 16-B load that bypasses the GPU caches (sc0 sc1: system coherence), from a
+// wave-uniform base + lane offset; offsets past the range read zeros.
+__device__ __forceinline__ uint4 ld_sys16(const void *base, uint32_t range, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)range, 0x00020000);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 1 | 16);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One request: body of len <= kSvcMaxLen bytes at V = body + 64*seg - len.
+template <uint32_t SEG>
+__device__ __forceinline__ uint32_t serve_crc0(const uint8_t *body, uint32_t len, uint32_t lane, uint32_t kshift) {
+  constexpr uint32_t kWords = SEG / 4;
+  const uint32_t off0 = 64u * SEG - len; // V offset of the body's first byte
+  uint32_t w[kWords];
+  if constexpr (SEG == 16) {
+    const uint4 v = ld_sys16(body, 64u * SEG, lane * 16u);
+    w[0] = v.x;
+    w[1] = v.y;
+    w[2] = v.z;
+    w[3] = v.w;
+  } else {
+#pragma unroll
+    for (uint32_t d = 0; d < kWords; ++d) w[d] = ld_sys32(reinterpret_cast<const uint32_t *>(body + lane * SEG) + d);
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (uint32_t d = 0; d < kWords; ++d) {
+    const uint32_t pos = lane * SEG + 4 * d;
+    const uint32_t keep = pos >= off0 ? 0xFFFFFFFFu : (pos + 4 <= off0 ? 0u : 0xFFFFFFFFu << (8 * (off0 - pos)));
+    s = crc0_word(s ^ (w[d] & keep));
+  }
+  // shift to V's end, then XOR over the wave
+  s = mulmod(s, kshift);
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) s ^= (uint32_t)__shfl_xor((int)s, m, 64);
+  return s;
+}
+
+__global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void crc32_service_kernel(SvcShared *sh, const uint32_t *tq,
+                                                                       const uint32_t *kshift, uint64_t idle_ticks,
+                                                                       uint64_t life_ticks, uint32_t instance) {
+  __shared__ uint32_t s_last;  // low 32 bits of the last request's s_memrealtime
+  __shared__ uint32_t s_alive; // waves still in the loop
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    s_last = (uint32_t)t_start;
+    s_alive = kSvcWaves;
+  }
+  __syncthreads();
+  // per-lane constants: shift of this lane's segment to V's end, per seg class
+  const uint32_t k4 = kshift[0 * 64 + lane], k8 = kshift[1 * 64 + lane], k16 = kshift[2 * 64 + lane];
+  const uint32_t slot0 = wave * kSvcPer;
+  // lane i < kSvcPer: the seq this wave last answered for slot slot0 + i
+  uint32_t served = 0;
+  if (lane < kSvcPer) served = (uint32_t)(__hip_atomic_load(&sh->res[slot0 + lane][0], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+  for (uint32_t poll = 0;; ++poll) {
+    const uint32_t seq = (lane < kSvcPer) ? ld_sys32(&sh->seq[slot0 + lane]) : 0u;
+    uint64_t pend = __builtin_amdgcn_ballot_w64(lane < kSvcPer && seq != served);
+    if (pend != 0) {
+      while (pend != 0) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1;
+        const uint32_t slot = slot0 + i;
+        const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)seq, (int)i);
+        const uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sys32(&sh->len[slot]));
+        uint32_t c0 = 0;
+        const uint8_t *body = sh->body[slot];
+        if (len <= 256u) c0 = serve_crc0<4>(body, len, lane, k4);
+        else if (len <= 512u) c0 = serve_crc0<8>(body, len, lane, k8);
+        else c0 = serve_crc0<16>(body, len <= kSvcMaxLen ? len : kSvcMaxLen, lane, k16);
+        const uint32_t crc = len == 0u ? 0u : ~(tq[len <= kSvcMaxLen ? len : 0u] ^ c0);
+        if (lane == 0)
+          __hip_atomic_store(&sh->res[slot][0], (uint64_t)crc | ((uint64_t)q << 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        served = (lane == i) ? q : served;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&s_last, (uint32_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      continue;
+    }
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    const uint32_t last = __hip_atomic_load(&s_last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    bool leave = (uint32_t)now - last > (uint32_t)idle_ticks || now - t_start > life_ticks;
+    if ((poll & 63u) == 63u) leave = leave || ld_sys32(&sh->ctl[kSvcStop]) != 0u;
+    if (leave) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  // the last wave out tells the host this instance is gone (a vector store)
+  if (lane == 0) {
+    const uint32_t left = __hip_atomic_fetch_sub(&s_alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (left == 1u) __hip_atomic_store(&sh->ctl[kSvcExited], instance, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+} // namespace
+
+hipError_t launch_service(SvcShared *sh, const uint32_t *tq, const uint32_t *kshift, uint64_t idle_ticks,
+                          uint64_t life_ticks, uint32_t instance, hipStream_t stream) {
+  hipLaunchKernelGGL(crc32_service_kernel, dim3(1), dim3(64 * kSvcWaves), 0, stream, sh, tq, kshift, idle_ticks,
+                     life_ticks, instance);
+  return hipGetLastError();
+}
+
+} // namespace rpccrc

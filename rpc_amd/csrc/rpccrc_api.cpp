@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <vector>
 
@@ -296,6 +297,22 @@ struct HostPipeline {
   bool ok = false;
 };
 
+// Drop-in service (crc32_service.hip): one resident workgroup answers drop-in
+// calls of <= kSvcMaxLen bytes through request slots in pinned coherent host
+// memory, so a call costs PCIe round trips instead of a kernel launch.
+struct Service {
+  SvcShared *sh = nullptr;     // pinned, coherent (hipHostMallocCoherent)
+  uint32_t *kshift = nullptr;  // device: 3 x 64 per-lane merge shifts
+  const uint32_t *tq = nullptr;
+  hipStream_t stream = nullptr;
+  std::mutex launch_mu;
+  uint32_t launched = 0;       // instances launched (under launch_mu); instance k stores k when it leaves
+  std::mutex slot_mu;
+  std::vector<int> free_slots; // under slot_mu
+  uint32_t seq[kSvcSlots] = {}; // last request seq of each slot (written by the slot's holder)
+  bool ok = false;
+};
+
 struct DeviceCtx {
   int device = -1;
   int cus = 0;
@@ -323,6 +340,8 @@ struct DeviceCtx {
   ObjPool<ScalarCtx> *scalar = nullptr;
   ObjPool<HostPipeline> *pipes = nullptr;
   StealPool *steal = nullptr;
+  Service *svc = nullptr;       // built on the first drop-in call (svc_once)
+  std::once_flag svc_once;
 };
 
 DeviceCtx g_dev[kMaxDevices];
@@ -918,6 +937,132 @@ uint32_t scalar_small(const DeviceCtx &c, ScalarCtx &t, const uint8_t *src, uint
   return (uint32_t)v;
 }
 
+// ---- drop-in service host side ---------------------------------
+
+// RPCCRC_SERVICE=0 turns the service off (every drop-in call launches a kernel).
+bool service_enabled() {
+  static const bool v = [] {
+    const char *e = getenv("RPCCRC_SERVICE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+constexpr uint64_t kSvcIdleTicks = 200000;   // 2 ms without a request (s_memrealtime, 100 MHz)
+constexpr uint64_t kSvcLifeTicks = 2000000;  // 20 ms per instance: bounds what a device-wide sync waits for
+constexpr uint64_t kSvcWaitNs = 2000000000;  // a call that gets no answer in 2 s is a device failure
+
+std::vector<Service *> g_services; // for the exit handler (under g_services_mu)
+std::mutex g_services_mu;
+
+// At process exit: ask every running instance to leave and wait (bounded) for
+// it, so no service wave outlives the process's last HIP call.
+void stop_services() {
+  std::lock_guard<std::mutex> g(g_services_mu);
+  for (Service *v : g_services) {
+    volatile uint32_t *ctl = v->sh->ctl;
+    ctl[kSvcStop] = 1u;
+    const uint64_t t0 = mono_ns();
+    while (ctl[kSvcExited] != v->launched && mono_ns() - t0 < 200000000ull) {
+    }
+  }
+}
+
+void svc_init(DeviceCtx &c) {
+  Service *v = new Service();
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(c.device);
+  hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&v->sh), sizeof(SvcShared), hipHostMallocCoherent);
+  if (e == hipSuccess) {
+    memset(v->sh, 0, sizeof(SvcShared));
+    std::vector<uint32_t> k(3 * 64);
+    const uint32_t segs[3] = {4, 8, 16};
+    for (int cl = 0; cl < 3; ++cl)
+      for (uint32_t L = 0; L < 64; ++L) k[cl * 64 + L] = gf2_xpow(8ull * segs[cl] * (63u - L));
+    e = hipMalloc(&v->kshift, k.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(v->kshift, k.data(), k.size() * 4, hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking);
+  (void)hipSetDevice(prev);
+  v->tq = c.tq;
+  for (int i = kSvcSlots - 1; i >= 0; --i) v->free_slots.push_back(i);
+  v->ok = e == hipSuccess;
+  if (v->ok) {
+    std::lock_guard<std::mutex> g(g_services_mu);
+    if (g_services.empty()) atexit(stop_services);
+    g_services.push_back(v);
+  }
+  c.svc = v;
+}
+
+bool svc_running(const Service &v) {
+  return *reinterpret_cast<const volatile uint32_t *>(&v.sh->ctl[kSvcExited]) != v.launched;
+}
+
+// Launches an instance unless one is running (the new one queues behind a
+// leaving one on the service stream).
+bool svc_ensure(DeviceCtx &c, Service &v) {
+  if (svc_running(v)) return true;
+  std::lock_guard<std::mutex> g(v.launch_mu);
+  if (svc_running(v)) return true;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  if (prev != c.device) (void)hipSetDevice(c.device);
+  const hipError_t e = launch_service(v.sh, v.tq, v.kshift, kSvcIdleTicks, kSvcLifeTicks, v.launched + 1, v.stream);
+  if (prev != c.device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) return false;
+  ++v.launched;
+  return true;
+}
+
+// One drop-in CRC through the service; false when the service is off, busy
+// (every slot held) or failed to launch -- the caller then launches a kernel.
+bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
+  if (!service_enabled() || len > kSvcMaxLen) return false;
+  std::call_once(c.svc_once, svc_init, std::ref(c));
+  Service &v = *c.svc;
+  if (!v.ok) return false;
+  int slot = -1;
+  {
+    std::lock_guard<std::mutex> g(v.slot_mu);
+    if (v.free_slots.empty()) return false;
+    slot = v.free_slots.back();
+    v.free_slots.pop_back();
+  }
+  SvcShared *sh = v.sh;
+  const uint32_t seg = len <= 256u ? 4u : len <= 512u ? 8u : 16u;
+  memcpy(sh->body[slot] + 64u * seg - len, src, len);
+  reinterpret_cast<volatile uint32_t *>(sh->len)[slot] = len;
+  uint32_t q = ++v.seq[slot];
+  if (q == 0) q = ++v.seq[slot]; // 0: the answered seq of a fresh slot
+  std::atomic_thread_fence(std::memory_order_release); // body and len before seq (x86: a compiler barrier)
+  reinterpret_cast<volatile uint32_t *>(sh->seq)[slot] = q;
+  bool ok = svc_ensure(c, v);
+  const volatile uint64_t *res = &sh->res[slot][0];
+  uint64_t r = *res;
+  if (ok && (uint32_t)(r >> 32) != q) {
+    const uint64_t t0 = mono_ns();
+    for (uint32_t spin = 1;; ++spin) {
+      r = *res;
+      if ((uint32_t)(r >> 32) == q) break;
+      if ((spin & 63u) == 0) {
+        // an instance that left just before our request: start the next one
+        if (!svc_ensure(c, v)) {
+          ok = false;
+          break;
+        }
+        if ((spin & 4095u) == 0 && mono_ns() - t0 > kSvcWaitNs) die("drop-in service (no answer)", RPCCRC_EIO);
+      }
+    }
+  }
+  {
+    std::lock_guard<std::mutex> g(v.slot_mu);
+    v.free_slots.push_back(slot);
+  }
+  if (ok) *crc = (uint32_t)r;
+  return ok;
+}
+
 // One CRC through the GPU.  The context (stream + staging) is borrowed from
 // the device's pool for the call: concurrent callers get distinct contexts,
 // and a context is reused by the next call of any thread.
@@ -925,6 +1070,8 @@ uint32_t scalar_crc(const void *data, uint32_t len) {
   DeviceCtx *c = nullptr;
   int rc = get_ctx(&c);
   if (rc) die("device init", rc);
+  uint32_t svc_r = 0;
+  if (svc_crc(*c, static_cast<const uint8_t *>(data), len, &svc_r)) return svc_r;
   ScalarCtx *t = c->scalar->acquire();
   if ((rc = scalar_ctx_init(*t))) die("scalar context", rc);
   const uint8_t *src = static_cast<const uint8_t *>(data);

@@ -830,3 +830,56 @@ def test_c3_per_rank_shard_full_coverage():
         bad = np.flatnonzero(got[lo:lo + step] != want)
         assert bad.size == 0, f"{bad.size} mismatches, first body {lo + int(bad[0])}"
         del part
+
+
+def test_drop_in_service_beside_batches():
+    """The drop-in service (crc32_service.hip, one resident workgroup with no LDS
+    table) must share the chip with the rows kernel's persistent grid (one
+    155 KiB-LDS workgroup per CU): north-star-sized batches while another thread
+    keeps the service busy run at about their normal time (a workgroup that could
+    not be placed would double it), and every CRC of both is exact."""
+    import time
+    n, L = 1 << 18, 4096
+    x = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(x, 0x5E7)
+    want = oracle.crc32_uniform(x.cpu().numpy(), n, L)
+    bodies = [oracle.splitmix_bytes(k, 0xD0 + k) for k in (12, 68, 300, 1000, 1024)]
+    wants = [oracle.crc32(b) for b in bodies]
+
+    def timed(reps=20):
+        s = torch.cuda.current_stream()
+        rpc_amd.device_uniform(x, n, L)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            out = rpc_amd.device_uniform(x, n, L)
+        e1.record(s)
+        e1.synchronize()
+        assert np.array_equal(u32(out), want)
+        return e0.elapsed_time(e1) / reps
+
+    alone = min(timed() for _ in range(3))
+    errors, calls = [], [0]
+    stop = threading.Event()
+
+    def hammer():
+        while not stop.is_set():
+            for b, w in zip(bodies, wants):
+                if rpc_amd.rpc_crc32(b) != w:
+                    errors.append(len(b))
+                calls[0] += 1
+
+    th = threading.Thread(target=hammer)
+    th.start()
+    try:
+        time.sleep(0.05)
+        busy = min(timed() for _ in range(3))
+    finally:
+        stop.set()
+        th.join()
+    print(f"rows batch alone {alone * 1e3:.1f} us, beside the drop-in service {busy * 1e3:.1f} us, "
+          f"{calls[0]} drop-in calls")
+    assert not errors, errors
+    assert calls[0] > 100
+    assert busy < 1.3 * alone, (alone, busy)
