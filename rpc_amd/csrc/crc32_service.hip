@@ -39,41 +39,11 @@
 #include "crc32_gf2.h"
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
+#include "crc32_service_math.h"
 
 namespace rpccrc {
 
 namespace {
-
-// crc0 of one 32-bit word x (state already XORed in): the bit loop
-// x = x * x (mod P) 32 times, 3 VALU per bit and one constant (a table of the
-// 32 single-bit results takes 2 VALU per bit but keeps 32 constants live).
-__device__ __forceinline__ uint32_t crc0_word(uint32_t x) {
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)x, 0, 1); // all ones iff bit 0
-    x = __builtin_amdgcn_bitop3_b32(x >> 1, lo, kPoly, 0x6A);         // (x >> 1) ^ (lo & P)
-  }
-  return x;
-}
-
-// a * b mod P, bit-serial over a (reflected: bit 31 = x^0).  `a` is shifted
-// along rather than tested bit by bit: independent bit tests were all hoisted
-// (one live VGPR each).
-__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b) {
-  uint32_t p = 0;
-  // b's powers b * x^i do not depend on a: without this barrier they were
-  // precomputed outside the poll loop, 32 live VGPRs per size class
-  __asm__ volatile("" : "+v"(b));
-#pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const uint32_t m = (uint32_t)((int32_t)a >> 31);
-    a <<= 1;
-    p = __builtin_amdgcn_bitop3_b32(p, m, b, 0x6A); // p ^ (m & b)
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1);
-    b = __builtin_amdgcn_bitop3_b32(b >> 1, lo, kPoly, 0x6A); // b * x
-  }
-  return p;
-}
 
 // 16-B load that bypasses the GPU caches (sc0 sc1: system coherence), from a
 // wave-uniform base + lane offset; offsets past the range read zeros.
@@ -107,12 +77,11 @@ __device__ __forceinline__ uint32_t serve_crc0(const uint8_t *body, uint32_t len
   uint32_t s = 0;
 #pragma unroll
   for (uint32_t d = 0; d < kWords; ++d) {
-    const uint32_t pos = lane * SEG + 4 * d;
-    const uint32_t keep = pos >= off0 ? 0xFFFFFFFFu : (pos + 4 <= off0 ? 0u : 0xFFFFFFFFu << (8 * (off0 - pos)));
-    s = crc0_word(s ^ (w[d] & keep));
+    const uint32_t keep = svc::keep_mask(lane * SEG + 4 * d, off0);
+    s = svc::crc0_word(s ^ (w[d] & keep));
   }
   // shift to V's end, then XOR over the wave
-  s = mulmod(s, kshift);
+  s = svc::mulmod(s, kshift);
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) s ^= (uint32_t)__shfl_xor((int)s, m, 64);
   return s;
@@ -150,8 +119,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
         const uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sys32(&sh->len[slot]));
         uint32_t c0 = 0;
         const uint8_t *body = sh->body[slot];
-        if (len <= 256u) c0 = serve_crc0<4>(body, len, lane, k4);
-        else if (len <= 512u) c0 = serve_crc0<8>(body, len, lane, k8);
+        const uint32_t seg = svc::seg_of(len);
+        if (seg == 4u) c0 = serve_crc0<4>(body, len, lane, k4);
+        else if (seg == 8u) c0 = serve_crc0<8>(body, len, lane, k8);
         else c0 = serve_crc0<16>(body, len <= kSvcMaxLen ? len : kSvcMaxLen, lane, k16);
         const uint32_t crc = len == 0u ? 0u : ~(tq[len <= kSvcMaxLen ? len : 0u] ^ c0);
         if (lane == 0)

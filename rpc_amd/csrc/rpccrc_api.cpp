@@ -32,6 +32,7 @@
 #include "crc32_gf2.h"
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
+#include "crc32_service_math.h"
 #include "frames.h"
 
 namespace rpccrc {
@@ -1030,7 +1031,7 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
     v.free_slots.pop_back();
   }
   SvcShared *sh = v.sh;
-  const uint32_t seg = len <= 256u ? 4u : len <= 512u ? 8u : 16u;
+  const uint32_t seg = svc::seg_of(len);
   memcpy(sh->body[slot] + 64u * seg - len, src, len);
   reinterpret_cast<volatile uint32_t *>(sh->len)[slot] = len;
   uint32_t q = ++v.seq[slot];

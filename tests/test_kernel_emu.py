@@ -82,3 +82,27 @@ def test_edge_fix_matches_byte_mask(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("ok ")
+
+
+def _mix(z):
+    M = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
+
+
+def test_service_lane_algebra_matches_zlib(tmp_path):
+    """The drop-in service kernel's arithmetic (rpc_amd/csrc/crc32_service_math.h,
+    compiled for the host with the gfx950 bitop3 / sbfe immediates emulated bit for
+    bit) equals zlib crc32 for every length 1..1024 -- all three size classes, stale
+    staging bytes before the body masked (tests/cpu_emu/service_emu.cpp)."""
+    import zlib
+    exe = str(tmp_path / "service_emu")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(REPO, "tests/cpu_emu/service_emu.cpp")],
+                   check=True)
+    lens = list(range(1, 1025))
+    out = subprocess.run([exe], input=(f"{len(lens)}\n" + "\n".join(map(str, lens))).encode(), capture_output=True,
+                         check=True).stdout.decode().split()
+    for k, (ln, got) in enumerate(zip(lens, out)):
+        body = bytes(_mix(0x5E17C0DE + k * 4096 + i) & 0xFF for i in range(ln))
+        assert int(got, 16) == zlib.crc32(body), ln
