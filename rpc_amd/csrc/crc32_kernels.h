@@ -76,7 +76,8 @@ constexpr uint64_t kBigMaxChunks = 1ull << 20;
 // per call on one box: 4080 B 622-634 us, 8176 B 590-596 us, 16368 B 602-609 us
 // (profiles/r03d/frames_chunks.txt); 16 KiB chunks until round 3.
 // The plan grows it as (chunk + 16) * 2 - 16 until the chunks fit kBigMaxChunks.
-constexpr uint64_t kBigMinChunk = 8192 - 16;
+constexpr uint64_t kBigMinChunk = 8192 - 16;       // end-aligned chunks (BigRoute.aligned = false)
+constexpr uint64_t kBigMinChunkAligned = 8192;     // address-aligned chunks (the default)
 struct BigRoute {
   uint32_t *routed;  // bit i: body i takes the route (ceil(n / 64) * 2 words, all written)
   uint64_t *meta;    // [0] bodies claimed, [1] their bytes, [2] chunks, [3] chunk bytes
@@ -85,7 +86,11 @@ struct BigRoute {
   uint64_t *c_off;   // kBigMaxChunks: chunk offsets / lengths / crc0
   uint32_t *c_len;
   uint32_t *c_raw;
-  uint64_t min_chunk = kBigMinChunk; // the plan's starting chunk size (power of two)
+  uint64_t min_chunk = kBigMinChunk; // the plan's starting chunk size (aligned: a power of two; else 2^k 4096 - 16)
+  // Address-aligned chunks (round 4): a body's pieces between multiples of the
+  // power-of-two chunk (interior chunks: whole aligned blocks, aligned rows).
+  // false: end-aligned chunks of 2^k * 4096 - 16 bytes (rounds 2-3).
+  bool aligned = true;
   // Route-all mode (all_n > 0): every body of a batch of all_n <= kBigMaxBodies
   // takes the route, body b = batch index b (no classify pass, no b_idx list,
   // no plain rows pass); the plan sums the lengths itself.

@@ -732,6 +732,171 @@ __global__ void __launch_bounds__(1024) big_combine_kernel(const uint32_t *lengt
   }
 }
 
+// ---- address-aligned chunks (round 4; BigRoute.aligned) ----------------------
+// The chunks of a routed body [s, e) (absolute addresses) are its pieces
+// between multiples of the power-of-two chunk C: [max(s, jC), min(e, jC + C)).
+// Interior chunks are then whole, aligned C-byte blocks: their rows are
+// aligned 4 KiB rows with no edge masks and no 128-B line shared with another
+// chunk.  End-aligned chunks of C - 16 bytes (rounds 2-3) put every row at an
+// arbitrary 16-B offset: 33 lines per 4 KiB row, the shared ones fetched twice,
+// and a front mask on every chunk.  The fold:
+//   crc = ~(A_t(G) ^ raw_last),  G = XOR_{k < nch-1} A_{(nch-2-k) C}(raw_k)
+// with raw_0 seeded with A_{len_0}(F) (zlib's pre-conditioning) and t the last
+// chunk's length; one chunk: crc = ~(raw_0 ^ A_{len_0}(F)).  Every map is a
+// power-of-two shift A_{2^k} (shift_nib), so no per-class tables are needed.
+__device__ __forceinline__ uint64_t aligned_nch(uint64_t s, uint64_t L, uint32_t lc) {
+  return L == 0 ? 0 : ((s + L - 1) >> lc) - (s >> lc) + 1;
+}
+
+__global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *base, const uint64_t *offsets,
+                                                                const uint32_t *lengths, BigRoute r) {
+  __shared__ unsigned long long wsum[16];
+  __shared__ unsigned long long run;
+  const uint64_t nb = big_count(r);
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  if (nb == 0) {
+    if (t == 0) {
+      r.meta[2] = 0;
+      r.meta[3] = r.min_chunk;
+    }
+    return;
+  }
+  uint64_t bytes;
+  if (r.all_n) {
+    unsigned long long x = 0;
+    for (uint64_t b = t; b < nb; b += 1024) x += lengths[b];
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    if (lane == 0) wsum[w] = x;
+    __syncthreads();
+    bytes = 0;
+    for (uint32_t k = 0; k < 16; ++k) bytes += wsum[k];
+    __syncthreads();
+  } else {
+    bytes = r.meta[1];
+  }
+  // sum over bodies of (L / C + 2) bounds the chunks
+  uint64_t chunk = r.min_chunk;
+  while (bytes / chunk + 2 * nb > kBigMaxChunks) chunk <<= 1;
+  const uint32_t lc = (uint32_t)__builtin_ctzll(chunk);
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  if (t == 0) run = 0;
+  __syncthreads();
+  for (uint64_t bb = 0; bb < nb; bb += 1024) {
+    const uint64_t b = bb + t;
+    unsigned long long c = 0;
+    if (b < nb) {
+      const uint32_t i = big_body(r, b);
+      c = aligned_nch(b0 + offsets[i], lengths[i], lc);
+    }
+    unsigned long long x = c; // inclusive wave scan
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    unsigned long long pre = run;
+    for (uint32_t k = 0; k < w; ++k) pre += wsum[k];
+    if (b < nb) r.b_first[b] = pre + x - c;
+    __syncthreads();
+    if (t == 1023) run = pre + x;
+    __syncthreads();
+  }
+  if (t == 0) {
+    r.b_first[nb] = run;
+    r.meta[2] = run;
+    r.meta[3] = chunk;
+  }
+}
+
+__global__ void __launch_bounds__(256) big_expand_aligned_kernel(const uint8_t *base, const uint64_t *offsets,
+                                                                 const uint32_t *lengths, BigRoute r) {
+  const uint64_t nb = big_count(r), chunk = r.meta[3];
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t i = big_body(r, b);
+    const uint64_t s = b0 + offsets[i], e = s + lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first;
+    const uint64_t blk0 = s & ~(chunk - 1);
+    for (uint64_t k = threadIdx.x; k < nch; k += 256) {
+      const uint64_t lo = blk0 + k * chunk;
+      const uint64_t cs = lo > s ? lo : s, ce = lo + chunk < e ? lo + chunk : e;
+      r.c_off[first + k] = cs - b0;
+      r.c_len[first + k] = (uint32_t)(ce - cs);
+    }
+  }
+}
+
+// Block b folds routed bodies b, b + grid, ...: thread t runs Horner over
+// chunks t, t + 1024, ... of the first nch - 1 with the step map A_{1024 C},
+// shifts its partial by A_{j C} (j < 1024 chunks after its last one), and the
+// block XOR-reduces into G; thread 0 adds the last chunk.  All maps are the
+// power-of-two shifts NIB[k] = A_{2^k bytes} (32 KiB, in LDS).
+__global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t *base, const uint64_t *offsets,
+                                                                   const uint32_t *lengths, BigRoute r,
+                                                                   const uint4 *shift_nib, uint32_t *out) {
+  __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
+  __shared__ uint32_t part[16];
+  const uint64_t nb = big_count(r);
+  if (blockIdx.x >= nb) return;
+  const uint32_t t = threadIdx.x;
+  const uint64_t chunk = r.meta[3];
+  const uint32_t lc = (uint32_t)__builtin_ctzll(chunk);
+  {
+    uint4 *dst = reinterpret_cast<uint4 *>(nib);
+#pragma unroll
+    for (uint32_t q = 0; q < kShiftNibWords / 4 / 1024; ++q) dst[q * 1024 + t] = shift_nib[q * 1024 + t];
+  }
+  __syncthreads();
+  auto apply = [&](uint64_t nbytes, uint32_t v) { // A_nbytes(v): one map per set bit
+    for (; nbytes; nbytes &= nbytes - 1) v = nib_map(nib + 128u * (uint32_t)__builtin_ctzll(nbytes), v);
+    return v;
+  };
+  const uint32_t *stepnib = nib + 128u * (lc + 10u); // A_{1024 C}
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t i = big_body(r, b);
+    const uint64_t s = b0 + offsets[i], L = lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first;
+    const uint64_t e = s + L;
+    // zlib's pre-conditioning, carried in by chunk 0 (thread 0): A_{len0}(F)
+    uint32_t seed = 0;
+    if (t == 0 && nch != 0) {
+      const uint64_t end0 = (s & ~(chunk - 1)) + chunk;
+      const uint64_t len0 = (end0 < e ? end0 : e) - s;
+      seed = apply(len0 & ~4095ull, r.tq[len0 & 4095u]); // A_{4096 q} after Tq[len0 mod 4096]
+    }
+    const uint64_t m = nch ? nch - 1 : 0; // chunks folded into G
+    uint32_t acc = 0;
+    constexpr uint32_t kB = 8;
+    for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * 1024u) {
+      uint32_t rv[kB];
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) rv[q] = (k0 + q * 1024u < m) ? r.c_raw[first + k0 + q * 1024u] : 0u;
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q)
+        if (k0 + q * 1024u < m) acc = nib_map(stepnib, acc) ^ rv[q] ^ (k0 + q == 0 ? seed : 0u);
+    }
+    if (t < m) { // chunks between this thread's last one and chunk m - 1
+      for (uint32_t j = (uint32_t)((m - 1 - t) % 1024u); j; j &= j - 1)
+        acc = nib_map(nib + 128u * (lc + (uint32_t)__builtin_ctz(j)), acc);
+    }
+    for (int d = 1; d < 64; d <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, d, 64);
+    if ((t & 63u) == 0) part[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) {
+      for (uint32_t w = 1; w < 16; ++w) acc ^= part[w];
+      uint32_t crc = 0;
+      if (nch == 1) {
+        crc = ~(r.c_raw[first] ^ seed);
+      } else if (nch > 1) {
+        const uint64_t last_lo = (e - 1) & ~(chunk - 1);
+        crc = ~(apply(e - last_lo, acc) ^ r.c_raw[first + nch - 1]);
+      }
+      out[i] = crc; // an empty body: crc32 = 0
+    }
+    __syncthreads();
+  }
+}
+
 } // namespace
 
 size_t big_route_workspace_bytes(uint64_t n) {
@@ -770,16 +935,29 @@ hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big
 hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,
                             hipStream_t s, uint32_t *steal, hipEvent_t steal_done, bool *steal_recorded) {
   if (proto.n_items == 0) return hipSuccess;
-  if (proto.mode != kModeFinal || proto.offsets == nullptr || proto.lengths == nullptr) return hipErrorInvalidValue;
-  // The fold indexes its maps by chunk class: chunk = 4096 * 2^m - 16 (the plan
-  // only doubles it), m < kBigChunkClasses; r.dbl / r.tq must be set.
-  const uint64_t p = r.min_chunk + 16;
-  if (p < 4096 || (p & (p - 1)) != 0 || (p >> 12) >= (1ull << kBigChunkClasses) || !r.dbl || !r.tq)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(big_plan_kernel, dim3(1), dim3(1024), 0, s, proto.lengths, r);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(big_expand_kernel, dim3(512), dim3(256), 0, s, proto.offsets, proto.lengths, r);
+  if (proto.mode != kModeFinal || proto.offsets == nullptr || proto.lengths == nullptr || !r.tq) return hipErrorInvalidValue;
+  hipError_t e;
+  if (r.aligned) {
+    // address-aligned power-of-two chunks (>= 4 KiB; the fold's step map is
+    // A_{1024 C}, so C <= 2^53)
+    if (r.min_chunk < 4096 || (r.min_chunk & (r.min_chunk - 1)) != 0 || r.min_chunk > (1ull << 40))
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(big_plan_aligned_kernel, dim3(1), dim3(1024), 0, s, proto.base, proto.offsets, proto.lengths, r);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(big_expand_aligned_kernel, dim3(512), dim3(256), 0, s, proto.base, proto.offsets, proto.lengths,
+                       r);
+  } else {
+    // The fold indexes its maps by chunk class: chunk = 4096 * 2^m - 16 (the plan
+    // only doubles it), m < kBigChunkClasses; r.dbl must be set.
+    const uint64_t p = r.min_chunk + 16;
+    if (p < 4096 || (p & (p - 1)) != 0 || (p >> 12) >= (1ull << kBigChunkClasses) || !r.dbl)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(big_plan_kernel, dim3(1), dim3(1024), 0, s, proto.lengths, r);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(big_expand_kernel, dim3(512), dim3(256), 0, s, proto.offsets, proto.lengths, r);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   ItemsArgs a = proto; // the chunks: rows kernel, RAW, count on the device
@@ -792,14 +970,18 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
   a.big_min = 0xFFFFFFFFu;
   a.mode = kModeRaw;
   a.out = r.c_raw;
-  // Two-row chunks (8176 B): the tail is dealt from the steal counter, the
-  // pool sized in the kernel from the device count (crc32_rows.h steal_s).
+  // The tail is dealt from the steal counter, the pool sized in the kernel
+  // from the device count (crc32_rows.h steal_s).
   a.steal = steal;
   e = launch_rows(a, 1, nt, max_blocks, s, steal_done, steal_recorded);
   if (e != hipSuccess) return e;
   // 1024 blocks (blocks past the routed-body count leave at once): a block folds
   // one body at a time, so the count bounds the serial bodies per block.
-  hipLaunchKernelGGL(big_combine_kernel, dim3(1024), dim3(1024), 0, s, proto.lengths, r, shift_nib, proto.out);
+  if (r.aligned)
+    hipLaunchKernelGGL(big_combine_aligned_kernel, dim3(1024), dim3(1024), 0, s, proto.base, proto.offsets,
+                       proto.lengths, r, shift_nib, proto.out);
+  else
+    hipLaunchKernelGGL(big_combine_kernel, dim3(1024), dim3(1024), 0, s, proto.lengths, r, shift_nib, proto.out);
   return hipGetLastError();
 }
 

@@ -379,15 +379,21 @@ uint32_t big_min_for(uint64_t n) {
   if (g_big_min_env) return g_big_min_env;
   return n <= kBigMaxBodies ? kBigMinSmallBatch : kBigMin;
 }
-// Chunk size the route starts from (it grows as (c + 16) * 2 - 16 until the
-// chunks fit kBigMaxChunks): 8176-byte two-row chunks deal with tail stealing
-// (launch_rows, device-counted).  Tuning override: RPCCRC_BIG_CHUNK
-// (2^k * 4096 - 16 bytes, e.g. 16368).
-const uint32_t g_big_chunk = [] {
+// Chunks of the big-body route: address-aligned power-of-two
+// chunks by default (RPCCRC_BIG_ALIGNED=0: the end-aligned 2^k * 4096 - 16-byte
+// chunks of rounds 2-3).  The plan doubles the size until the chunks fit
+// kBigMaxChunks.  Tuning override: RPCCRC_BIG_CHUNK (bytes: a power of two
+// >= 4096 aligned, 2^k * 4096 - 16 end-aligned).
+const bool g_big_aligned = [] {
+  const char *e = getenv("RPCCRC_BIG_ALIGNED");
+  return !(e && e[0] == '0');
+}();
+const uint64_t g_big_chunk = [] {
   const char *e = getenv("RPCCRC_BIG_CHUNK");
   const unsigned long long v = e ? strtoull(e, nullptr, 10) : 0ull;
+  if (g_big_aligned) return (v >= 4096 && v <= (1ull << 30) && (v & (v - 1)) == 0) ? (uint64_t)v : kBigMinChunkAligned;
   const unsigned long long p = v + 16;
-  return (v >= 4096 - 16 && p <= (1ull << 30) && (p & (p - 1)) == 0) ? (uint32_t)v : (uint32_t)kBigMinChunk;
+  return (v >= 4096 - 16 && p <= (1ull << 30) && (p & (p - 1)) == 0) ? (uint64_t)v : kBigMinChunk;
 }();
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kSplitMinFrames = 16384;       // fewer frames: one wave per body (rows kernel)
@@ -662,6 +668,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   if (route) {
     r = big_route_carve(ws.ptr() + split_bytes, n);
     r.min_chunk = g_big_chunk;
+    r.aligned = g_big_aligned;
     r.tq = c.tq;
     r.dbl = c.big_dbl;
     if (route_all) {

@@ -161,3 +161,51 @@ def test_big_fold_matches_zlib(L, chunk, nt):
     """The route's fold algebra (seeded chunk 0, doubling maps) equals zlib.crc32."""
     body = random.Random(L * 7 + chunk).randbytes(L)
     assert big_fold_emulated(body, chunk, nt) == zlib.crc32(body)
+
+
+# ---- address-aligned route chunks (big_*_aligned_kernel, DESIGN.md 4.6, round 4) ----
+# A body at absolute address s is cut at multiples of the power-of-two chunk C:
+# chunk k = [max(s, (s // C + k) C), min(e, (s // C + k + 1) C)).  The fold:
+#   G   = XOR_{k < nch-1} A_{(nch-2-k) C}(raw_k), raw_0 ^= A_{len0}(F), by the
+#         same thread-strided Horner (step A_{NT C}) and A_{j C} shifts;
+#   crc = ~(A_t(G) ^ raw_last), t = the last chunk's length; one chunk:
+#         crc = ~(raw_0 ^ A_{len0}(F)).
+
+
+def aligned_fold_emulated(body: bytes, start: int, chunk: int, nt: int) -> int:
+    L = len(body)
+    if L == 0:
+        return 0
+    s, e = start, start + L
+    nch = (e - 1) // chunk - s // chunk + 1
+    blk0 = s - s % chunk
+    pieces = [(max(s, blk0 + k * chunk), min(e, blk0 + (k + 1) * chunk)) for k in range(nch)]
+    raw = [crc0(body[a - s:b - s]) for a, b in pieces]
+    len0 = pieces[0][1] - pieces[0][0]
+    seed = nib_shift(len0 & ~4095, nib_shift(len0 & 4095, 0xFFFFFFFF))  # A_{4096 q}(Tq[len0 mod 4096])
+    if nch == 1:
+        return ~(raw[0] ^ seed) & 0xFFFFFFFF
+    m = nch - 1
+    g = 0
+    for t in range(nt):
+        acc, kk = 0, t
+        while kk < m:
+            acc = nib_shift(nt * chunk, acc) ^ raw[kk] ^ (seed if kk == 0 else 0)
+            kk += nt
+        if t < m:
+            acc = nib_shift(((m - 1 - t) % nt) * chunk, acc)
+        g ^= acc
+    t_last = pieces[-1][1] - pieces[-1][0]
+    return ~(nib_shift(t_last, g) ^ raw[-1]) & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("L,start,chunk,nt", [
+    (1, 0, 4096, 4), (1, 4095, 4096, 4), (2, 4095, 4096, 4), (4096, 0, 4096, 4), (4096, 16, 4096, 4),
+    (8192, 0, 8192, 8), (8193, 8191, 8192, 8), (9000, 5, 8192, 2), (5 * 8192 + 7, 12345, 8192, 4),
+    (40000, 100, 4096, 4), (33000, 16384 - 3, 16384, 1), (70000, 8192 * 3, 8192, 3),
+])
+def test_aligned_fold_matches_zlib(L, start, chunk, nt):
+    """The aligned route's chunking and fold algebra equal zlib.crc32 at any body
+    alignment (single chunk, body inside one block, head + interior + tail)."""
+    body = random.Random(L * 11 + start).randbytes(L)
+    assert aligned_fold_emulated(body, start, chunk, nt) == zlib.crc32(body)
