@@ -17,4 +17,6 @@ dev = torch.device("cuda:0")
 for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
     r = bench.frames_lifted_probe(dev)
     r["big_min"] = os.environ.get("RPCCRC_BIG_MIN", "default")
+    r["big_aligned"] = os.environ.get("RPCCRC_BIG_ALIGNED", "default")
+    r["big_chunk"] = os.environ.get("RPCCRC_BIG_CHUNK", "default")
     print(json.dumps(r), flush=True)

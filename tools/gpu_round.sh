@@ -62,6 +62,12 @@ for s in $STEPS; do
            for k in ${FRAMES_CHUNKS:-4080 8176 16368}; do
              RPCCRC_BIG_CHUNK=$k run frames_chunk$k 300 python tools/frames_lifted.py 3 || exit 1
            done ;;
+    frames_ab) # interleaved: end-aligned (0) vs address-aligned (1) route chunks, and 16 KiB aligned chunks
+           for i in 1 2; do
+             for v in "0 8176" "1 8192" "1 16384"; do set -- $v
+               RPCCRC_BIG_ALIGNED=$1 RPCCRC_BIG_CHUNK=$2 run frames_a$1_c$2_$i 300 python tools/frames_lifted.py 2 || exit 1
+             done
+           done ;;
     prof_frames) run prof_frames 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_frames" -o run --output-format csv -- \
                    python3 tools/frames_lifted.py 3 ;;
     ragged) run ragged_${RAGGED_CFG:-c2} 300 python tools/probe.py --mode ragged --config ${RAGGED_CFG:-c2} --rounds ${RAGGED_ROUNDS:-3} --reps 5 ;;
