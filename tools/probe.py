@@ -62,7 +62,7 @@ def lib_variants(w, a):
 def ablate_variants(w, a):
     """Rows-kernel variants: (qb, pair, nt, abl) -- abl bits 1 no-compute,
     2 no-merge, 4 no-load, 8 natural lane->piece load order."""
-    so = os.path.join(REPO, "tools", "libprobe.so")
+    so = os.environ.get("RPCCRC_PROBE_LIB", os.path.join(REPO, "tools", "libprobe.so"))
     if not os.path.exists(so):
         subprocess.run(["make", "-C", os.path.join(REPO, "tools")], check=True)
     lib = ctypes.CDLL(so)
@@ -117,7 +117,7 @@ def timeline(w, a):
     product kernel (kRowsAblTimes variant, exact results) after a clock prewarm:
     how much of a launch is fill (launch spread + image copy) and drain (exit spread)."""
     import time
-    so = os.path.join(REPO, "tools", "libprobe.so")
+    so = os.environ.get("RPCCRC_PROBE_LIB", os.path.join(REPO, "tools", "libprobe.so"))
     if not os.path.exists(so):
         subprocess.run(["make", "-C", os.path.join(REPO, "tools")], check=True)
     lib = ctypes.CDLL(so)
@@ -233,7 +233,7 @@ def ragged_ablate(a):
     the quarter / half first rows.  Interleaved rounds, median; exact variants
     (0, 16384) are checked against the product's CRCs."""
     import time
-    so = os.path.join(REPO, "tools", "libprobe.so")
+    so = os.environ.get("RPCCRC_PROBE_LIB", os.path.join(REPO, "tools", "libprobe.so"))
     lib = ctypes.CDLL(so)
     lib.probe_rows_ragged.restype = ctypes.c_int
     lib.probe_rows_ragged.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
@@ -280,7 +280,7 @@ def stream_rows(a):
     mode, GB/s and tiles (wave iterations) per us over the north-star buffer,
     after a clock prewarm, interleaved rounds."""
     import time
-    so = os.path.join(REPO, "tools", "libprobe.so")
+    so = os.environ.get("RPCCRC_PROBE_LIB", os.path.join(REPO, "tools", "libprobe.so"))
     lib = ctypes.CDLL(so)
     lib.probe_stream_rows.restype = ctypes.c_int
     lib.probe_stream_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
