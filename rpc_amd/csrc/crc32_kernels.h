@@ -129,14 +129,13 @@ hipError_t launch_scalar(const uint8_t *stage, uint32_t len, const uint4 *tab, c
 // ---- drop-in service (crc32_service.hip) ---------------------
 // A resident one-workgroup kernel answers drop-in calls of <= kSvcMaxLen bytes
 // through request slots in pinned, coherent host memory: no launch per call.
-constexpr uint32_t kSvcWaves = 4;                      // waves of the service workgroup
-constexpr uint32_t kSvcPer = 4;                        // slots per wave
+constexpr uint32_t kSvcWaves = 8;                      // waves of the service workgroup (2 per SIMD)
+constexpr uint32_t kSvcPer = 2;                        // slots per wave: wave w owns slots w + 8 i
 constexpr uint32_t kSvcSlots = kSvcWaves * kSvcPer;    // concurrent drop-in calls served
 constexpr uint32_t kSvcMaxLen = 1024;                  // MAX_BODY_LEN (rpc.h:17)
 constexpr uint32_t kSvcStop = 0, kSvcExited = 1;       // SvcShared::ctl words
 struct SvcShared {
-  uint32_t seq[kSvcSlots];            // host: request sequence of each slot (written last)
-  uint32_t len[kSvcSlots];            // host: body length
+  uint64_t req[kSvcSlots];            // host: {len (low), seq (high)} of each slot, one store, after the body
   uint64_t res[kSvcSlots][8];         // device: {crc, seq} (crc in the low half), one 64-B line per slot
   uint32_t ctl[16];                   // [kSvcStop] host: leave now; [kSvcExited] device: last instance that left
   uint8_t body[kSvcSlots][kSvcMaxLen]; // host: the body, right-aligned in 64 * seg bytes (seg 4 / 8 / 16)

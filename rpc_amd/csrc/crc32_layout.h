@@ -75,6 +75,22 @@ static_assert(kLdsBytesV3 % 16 == 0 && kLdsBytesV3 <= 163840, "fits the 160 KiB 
 constexpr uint32_t sq_byte(uint32_t j, uint32_t n, uint32_t nib) { return kLdsSQ + n * 256u + j * 64u + nib * 4u; }
 void build_lds_image_v2(uint32_t *img /* kLdsBytesV3 bytes: V2 + the SQ tables */);
 
+// Compact HBM form of the image (round 4): MAIN is 32 copies of the four
+// slice-by-4 tables, so HBM holds them once -- word tbl * 256 + v, tbl = 0..3
+// for T3, T2, T1, T0 (MAIN's regions / halves in order) -- followed by the
+// image bytes from kLdsST1 on.  Each workgroup reads ~38 KiB instead of 157 KiB
+// and writes the 128 KiB of copies into LDS itself (crc32_rows.h
+// img_load / img_store): 256 workgroups had read 40 MB from L2 per launch.
+// RPCCRC_IMG_COMPACT=0 keeps the full 157 KiB image in HBM (A/B only).
+#ifndef RPCCRC_IMG_COMPACT
+#define RPCCRC_IMG_COMPACT 1
+#endif
+constexpr bool kImgCompact = RPCCRC_IMG_COMPACT != 0;
+constexpr uint32_t kImgTailOfs = 4096; // compact form: where image byte kLdsST1 sits
+constexpr uint32_t kImgCompactBytes = kImgTailOfs + (kLdsBytesV3 - kLdsST1);
+constexpr uint32_t kImgHbmBytes = kImgCompact ? kImgCompactBytes : kLdsBytesV3; // what the device context uploads
+void build_lds_image_compact(const uint32_t *img /* kLdsBytesV3 bytes */, uint32_t *compact /* kImgCompactBytes */);
+
 // Host-side builder (crc32_tables.cpp).
 void build_tq(uint32_t *tq /* kTqEntries */);
 

@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_packed_kernel(PackedArgs a) {
   // are walked by one CU at about the same time.
   __shared__ uint32_t s_grab;
   if (threadIdx.x == 0) s_grab = 0;
-  copy_lds_image<kLdsBytesV2>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
+  copy_lds_image<kLdsBytesV2>(a.lds_image, s_lds);
   __syncthreads();
   const uint8_t *lds = reinterpret_cast<const uint8_t *>(s_lds);
 

@@ -246,23 +246,70 @@ __device__ __forceinline__ uint32_t swap_lanebit4(uint32_t v, bool upper) {
   return upper ? a[0] : a[1];
 }
 
-// Workgroup copy of the kBytes LDS table image (1024 threads): all of a
-// thread's global loads in flight at once, then the LDS stores.  Whole
-// iterations and the one partial iteration are separate so that every value
+// Workgroup copy of the kBytes LDS table image (1024 threads) from its HBM
+// form (crc32_layout.h kImgCompact): img_load issues all of a thread's global
+// loads at once into registers, img_store writes LDS.  Compact form: the
+// thread's 8 MAIN pieces (16 B = 4 copies of one table word each; lanes of a
+// wave write consecutive pieces, so the stores are bank-conflict-free) come
+// from 8 dword loads of the 4 KiB single-copy tables, the rest of the image is
+// copied.  Whole iterations and the partial one are separate so every value
 // stays in a register (a conditionally written local array went to scratch:
 // 176 B per lane, the image loaded twice).
 template <uint32_t kBytes>
-__device__ __forceinline__ void copy_lds_image(const uint4 *src, uint4 *dst) {
-  constexpr uint32_t kN16 = kBytes / 16, kFull = kN16 / 1024, kRem = kN16 % 1024;
+struct ImgRegs {
+  static constexpr uint32_t kTail = (kBytes - kLdsST1) / 16, kTailIt = (kTail + 1023) / 1024; // compact
+  static constexpr uint32_t kFull = kBytes / 16 / 1024, kRem = (kBytes / 16) % 1024;          // full
+  uint32_t t[kImgCompact ? 8 : 1];
+  u32x4 p[kImgCompact ? kTailIt : kFull + 1];
+};
+template <uint32_t kBytes>
+__device__ __forceinline__ void img_load(const uint4 *src, ImgRegs<kBytes> &r) {
+  using R = ImgRegs<kBytes>;
   const uint32_t tid = threadIdx.x;
-  uint4 t[kFull];
+  if constexpr (kImgCompact) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(src);
 #pragma unroll
-  for (uint32_t i = 0; i < kFull; ++i) t[i] = src[tid + i * 1024u];
-  uint4 r = make_uint4(0, 0, 0, 0);
-  if (kRem != 0 && tid < kRem) r = src[kFull * 1024u + tid];
+    for (uint32_t k = 0; k < 8; ++k) { // MAIN piece q: region q >> 12, row (q >> 4) & 255, half (q >> 3) & 1
+      const uint32_t q = tid + 1024u * k;
+      r.t[k] = w[(((q >> 12) << 1) | ((q >> 3) & 1u)) * 256u + ((q >> 4) & 255u)];
+    }
+    const u32x4 *tail = reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(src) + kImgTailOfs);
 #pragma unroll
-  for (uint32_t i = 0; i < kFull; ++i) dst[tid + i * 1024u] = t[i];
-  if (kRem != 0 && tid < kRem) dst[kFull * 1024u + tid] = r;
+    for (uint32_t i = 0; i < R::kTailIt; ++i) {
+      const uint32_t q = tid + 1024u * i;
+      r.p[i] = (i + 1 < R::kTailIt || q < R::kTail) ? tail[q] : u32x4{0u, 0u, 0u, 0u};
+    }
+  } else {
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src);
+#pragma unroll
+    for (uint32_t i = 0; i < R::kFull; ++i) r.p[i] = s4[tid + i * 1024u];
+    r.p[R::kFull] = (R::kRem != 0 && tid < R::kRem) ? s4[R::kFull * 1024u + tid] : u32x4{0u, 0u, 0u, 0u};
+  }
+}
+template <uint32_t kBytes>
+__device__ __forceinline__ void img_store(const ImgRegs<kBytes> &r, uint32_t *lds) {
+  using R = ImgRegs<kBytes>;
+  const uint32_t tid = threadIdx.x;
+  u32x4 *d4 = reinterpret_cast<u32x4 *>(lds);
+  if constexpr (kImgCompact) {
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) d4[tid + 1024u * k] = u32x4{r.t[k], r.t[k], r.t[k], r.t[k]};
+#pragma unroll
+    for (uint32_t i = 0; i < R::kTailIt; ++i) {
+      const uint32_t q = tid + 1024u * i;
+      if (i + 1 < R::kTailIt || q < R::kTail) d4[kLdsST1 / 16u + q] = r.p[i];
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < R::kFull; ++i) d4[tid + i * 1024u] = r.p[i];
+    if (R::kRem != 0 && tid < R::kRem) d4[R::kFull * 1024u + tid] = r.p[R::kFull];
+  }
+}
+template <uint32_t kBytes>
+__device__ __forceinline__ void copy_lds_image(const uint4 *src, uint32_t *dst) {
+  ImgRegs<kBytes> r;
+  img_load<kBytes>(src, r);
+  img_store<kBytes>(r, dst);
 }
 
 // Read-only kernel inputs through the constant address space: uniform indices
@@ -580,25 +627,6 @@ constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
 #define RPCCRC_STEAL_AHEAD 1
 #endif
 constexpr uint32_t kStealAhead = RPCCRC_STEAL_AHEAD;
-// Pool UNITS per dealing round (1, 2 or 4): the pool is claimed in units of
-// kRound / kStealSplit tasks, kStealSplit * kStealAhead units ahead (the same
-// lead time).  When the pool runs dry a workgroup still holds at most its
-// current unit plus the claimed-ahead ones, so smaller units shorten the
-// launch's drain (C1: ~12 us of exit spread with whole-round claims,
-// profiles/r03h/timeline_steal_c1.log).  A static round still completes as one
-// unit; a pool round completes per unit (its own done count and store), and
-// its ring slot is freed when all of its units are stored.
-#ifndef RPCCRC_STEAL_SPLIT
-#define RPCCRC_STEAL_SPLIT 1
-#endif
-constexpr uint32_t kStealSplit = RPCCRC_STEAL_SPLIT;
-static_assert(kStealSplit == 1 || kStealSplit == 2 || kStealSplit == 4, "pool units per round: 1, 2 or 4");
-#ifndef RPCCRC_STEAL_AHEAD_UNITS
-#define RPCCRC_STEAL_AHEAD_UNITS (RPCCRC_STEAL_AHEAD * RPCCRC_STEAL_SPLIT)
-#endif
-constexpr uint32_t kStealAheadUnits = RPCCRC_STEAL_AHEAD_UNITS;
-static_assert(kStealAheadUnits >= 1 && kStealAheadUnits <= kStealAhead * kStealSplit,
-              "claims at most kStealAhead rounds ahead (the host sizes steal_s >= kStealAhead)");
 constexpr uint32_t kStealQ = 16;                      // LDS queue ring
 constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
 // Bounded waits.  Both waits end by protocol (a claim is published by the wave
@@ -608,26 +636,27 @@ constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, t
 // stores kErrStealWait / kErrRingWait into the launch's error word a.err and
 // moves on -- the host then reports RPCCRC_EIO instead of returning stale CRCs
 // silently (VERDICT / ADVICE r02), and no wait can turn into a hang.
-// The cap is wall time (s_memrealtime, 100 MHz), not a spin count: a ring slot
-// waits for the slowest task of the round 8 rounds back, and one task may be a
-// body of up to 4 GiB walked by ONE wave (a ragged batch whose length bound
-// skips the big-body route) -- ~1-3 s at one wave's rate.  Round 3's cap of
-// 2^21 sleeps (~0.1 s) fired on such a healthy launch.
-constexpr uint64_t kWaitCapTicks = 30ull * 100000000ull; // 30 s
-// Lane 0's wait-loop clock: the first call (spin 0) starts it, later calls
-// report whether the cap has passed.
-__device__ __forceinline__ bool wait_expired(uint32_t spin, uint64_t &t0) {
-  const uint64_t now = __builtin_amdgcn_s_memrealtime();
-  if (spin == 0) t0 = now;
-  return now - t0 > kWaitCapTicks;
+// The cap must outlast any healthy wait: a ring slot waits for the slowest
+// task of the round 8 rounds back, and one task may be a body of up to 4 GiB
+// walked by ONE wave (a ragged batch whose length bound skips the big-body
+// route) -- ~1-3 s at one wave's rate.  Round 3's cap of 2^21 short sleeps
+// (~0.1 s) fired on such a healthy launch.  The first 1024 spins
+// sleep briefly (a healthy wait is usually microseconds), later ones
+// s_sleep 127 (~8K cycles, >= 3.4 us): 2^23 spins are >= ~28 s.  (A wall-time
+// cap from s_memrealtime kept 64-bit timestamps live: SGPR spills in the hot
+// loops went 2 -> 7 on the north-star kernel.)
+constexpr uint32_t kWaitSpinMax = 1u << 23;
+__device__ __forceinline__ bool wait_spin(uint32_t spin) { // sleeps; true once the cap has passed
+  if (spin >= kWaitSpinMax) return true;
+  if (spin < 1024u) __builtin_amdgcn_s_sleep(2);
+  else __builtin_amdgcn_s_sleep(127);
+  return false;
 }
-// DYN control block: [0] task counter, kDynSlots * kStealSplit unit done
-// counts, kDynSlots slot generations, kDynSlots stored-unit counts (split pool
-// rounds only), then the CRC ring (QB CRCs per task, kRound tasks per slot).
-constexpr uint32_t dyn_done_words(int QB) { return dyn_slots(QB) * kStealSplit; }
-constexpr uint32_t dyn_gen_ofs(int QB) { return 1 + dyn_done_words(QB); }
-constexpr uint32_t dyn_stored_ofs(int QB) { return dyn_gen_ofs(QB) + dyn_slots(QB); }
-constexpr uint32_t dyn_ringbuf_ofs(int QB) { return dyn_stored_ofs(QB) + (kStealSplit > 1 ? dyn_slots(QB) : 0u); }
+// DYN control block: [0] task counter, kDynSlots done counts, kDynSlots slot
+// generations (slot s starts at round s), then the CRC ring (QB CRCs per task,
+// kRound tasks per slot).
+constexpr uint32_t dyn_gen_ofs(int QB) { return 1 + dyn_slots(QB); }
+constexpr uint32_t dyn_ringbuf_ofs(int QB) { return dyn_gen_ofs(QB) + dyn_slots(QB); }
 constexpr uint32_t dyn_ring_words(int QB) { return dyn_ringbuf_ofs(QB) + dyn_slots(QB) * dyn_round(QB) * (uint32_t)QB; }
 constexpr uint32_t dyn_ctl_words(int QB) { return dyn_ring_words(QB) + kStealCtlWords; }
 
@@ -638,15 +667,14 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   static_assert(!STEAL || DYN, "stealing: DYN launches");
   constexpr uint32_t kRound = dyn_round(QB); // tasks per dealing round
   constexpr uint32_t kDynSlots = dyn_slots(QB);
-  constexpr uint32_t kUnit = kRound / kStealSplit; // tasks per pool unit (tail stealing)
-  constexpr uint32_t kGen = dyn_gen_ofs(QB), kStored = dyn_stored_ofs(QB), kRingBuf = dyn_ringbuf_ofs(QB);
+  constexpr uint32_t kGen = dyn_gen_ofs(QB), kRingBuf = dyn_ringbuf_ofs(QB);
   // sub-row first rows: ragged QB = 1 with the plain chain (image V3 adds SQ)
   constexpr bool kSub = kSubRows && QB == 1 && RAGGED && !kTwoChains &&
                         (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblHalfChain | kRowsAblNoSub)) == 0;
   constexpr uint32_t kImgBytes = kSub ? kLdsBytesV3 : kLdsBytesV2;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kImgBytes / 4];
-  // DYN control block (dyn_ring_words): task counter, unit done counts, slot
-  // generations (slot s starts at round s), stored-unit counts, CRC ring.
+  // DYN control block (dyn_ring_words): task counter, done counts, slot
+  // generations (slot s starts at round s), CRC ring.
   __shared__ uint32_t s_ctl[DYN ? (STEAL ? dyn_ctl_words(QB) : dyn_ring_words(QB)) : 1];
   // kEarlyRow: each wave's first task is static (DYN: counter index = wave, so
   // the LDS counter starts at 16), and its first row's loads are issued between
@@ -655,8 +683,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   constexpr bool kEarly = kEarlyRow && (ABL & kRowsAblTimes) == 0;
   if constexpr (DYN) {
     if (threadIdx.x < kRingBuf)
-      s_ctl[threadIdx.x] = (threadIdx.x >= kGen && threadIdx.x < kStored) ? threadIdx.x - kGen
-                                                                          : ((threadIdx.x == 0u && kEarly) ? 16u : 0u);
+      s_ctl[threadIdx.x] = (threadIdx.x >= kGen) ? threadIdx.x - kGen : ((threadIdx.x == 0u && kEarly) ? 16u : 0u);
     if (STEAL && threadIdx.x < 3 + kStealQ) s_ctl[dyn_ring_words(QB) + threadIdx.x] = 0u; // tail/done/inflight/tags
   }
   // Device-side item counts (split lists, big-body chunks) may be 0: leave
@@ -667,23 +694,16 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   // All of this thread's image loads in flight at once (a rolled loop would
   // pay one L2 round trip per 16 KiB before the first HBM byte is read).
-  constexpr uint32_t kImgFull = kImgBytes / 16 / 1024, kImgRem = (kImgBytes / 16) % 1024;
   // kEarly: the image in registers until the first row's loads are issued
   // (native vectors: HIP's uint4 struct copies became memcpys through a
   // private-memory array -- 160 B of scratch per lane).
-  using img_v = unsigned int __attribute__((ext_vector_type(4)));
-  const img_v *img_src = reinterpret_cast<const img_v *>(a.lds_image);
-  img_v *img_dst = reinterpret_cast<img_v *>(s_lds);
-  img_v img_t[kEarly ? kImgFull : 1];
-  img_v img_r = img_v{0u, 0u, 0u, 0u};
+  ImgRegs<kImgBytes> img;
   if constexpr (!kEarly) {
-    if constexpr ((ABL & kRowsAblNoImage) == 0) copy_lds_image<kImgBytes>(a.lds_image, reinterpret_cast<uint4 *>(s_lds));
+    if constexpr ((ABL & kRowsAblNoImage) == 0) copy_lds_image<kImgBytes>(a.lds_image, s_lds);
     __syncthreads();
     if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();
   } else if constexpr ((ABL & kRowsAblNoImage) == 0) {
-#pragma unroll
-    for (uint32_t i = 0; i < kImgFull; ++i) img_t[i] = img_src[threadIdx.x + i * 1024u];
-    if (kImgRem != 0 && threadIdx.x < kImgRem) img_r = img_src[kImgFull * 1024u + threadIdx.x];
+    img_load<kImgBytes>(a.lds_image, img);
   }
   // LDS stores of the image + the barrier (kEarly: after the first row's loads
   // are issued; the loads above were issued first, so waiting for them does
@@ -694,10 +714,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 #define RPCCRC_ROWS_IMAGE_READY()                                                                          \
   do {                                                                                                     \
     __builtin_amdgcn_sched_barrier(0);                                                                     \
-    if constexpr ((ABL & kRowsAblNoImage) == 0) {                                                          \
-      _Pragma("unroll") for (uint32_t i = 0; i < kImgFull; ++i) img_dst[threadIdx.x + i * 1024u] = img_t[i]; \
-      if (kImgRem != 0 && threadIdx.x < kImgRem) img_dst[kImgFull * 1024u + threadIdx.x] = img_r;           \
-    }                                                                                                      \
+    if constexpr ((ABL & kRowsAblNoImage) == 0) img_store<kImgBytes>(img, s_lds);                          \
     __syncthreads();                                                                                       \
     if constexpr ((ABL & kRowsAblTimes) != 0) t_image = __builtin_amdgcn_s_memrealtime();                  \
   } while (0)
@@ -781,7 +798,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   }();
   const bool steal = STEAL && steal_s != 0u;
   const uint32_t pool_first = steal_s * nblk; // first pool (global) round
-  const uint32_t pool_n = steal ? (n_tasks + kUnit - 1) / kUnit - pool_first * kStealSplit : 0u; // pool units
+  const uint32_t pool_n = steal ? (n_tasks + kRound - 1) / kRound - pool_first : 0u;
   uint32_t *q_ctl = s_ctl + (STEAL ? dyn_ring_words(QB) : 0u);
   uint32_t *q_tail = q_ctl, *q_done = q_ctl + 1, *q_inflight = q_ctl + 2;
   uint32_t *q_tag = q_ctl + 3, *q_id = q_ctl + 3 + kStealQ;
@@ -794,13 +811,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   };
   // Lane 0: wait until output-ring slot `slot` is free for round `rnd` (bounded).
   auto ring_wait = [&](const uint32_t *gen, uint32_t slot, uint32_t rnd) {
-    uint64_t t0 = 0;
     for (uint32_t spin = 0; __hip_atomic_load(&gen[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != rnd; ++spin) {
-      if (wait_expired(spin, t0)) {
+      if (wait_spin(spin)) {
         report_err(kErrRingWait);
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
     }
   };
   auto lds_ld_acq = [](uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
@@ -822,10 +837,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     }
     has_claim = false;
   };
-  // The wave taking a local unit's first task claims a pool unit for the
-  // workgroup (for use kStealAheadUnits units later).
+  // The wave taking local round r's first task claims a pool round for the
+  // workgroup (for use kStealAhead rounds later).
   auto claim_if_first = [&](uint32_t c) { // uniform
-    if (!steal || c % kUnit != 0u || c / kUnit + kStealAheadUnits < steal_s * kStealSplit) return;
+    if (!steal || c % kRound != 0u || c / kRound + kStealAhead < steal_s) return;
     publish(); // at most one claim in flight per wave
     uint32_t go = 0;
     if (lane == 0 && lds_ld_acq(q_done) == 0u) {
@@ -845,13 +860,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     const uint32_t r = c / kRound;
     more = true;
     if (!steal || r < steal_s) return dyn_task(c);
-    const uint32_t q = c / kUnit - steal_s * kStealSplit, k = q % kStealQ; // the workgroup's q-th pool unit
+    const uint32_t q = r - steal_s, k = q % kStealQ;
     if (a.test_giveup != 0u) { // test-only: take the give-up path below deterministically
       if (lane == 0) report_err(kErrStealWait);
       more = false;
       return n_tasks;
     }
-    uint64_t t0 = 0;
     for (uint32_t spin = 0;; ++spin) {
       uint32_t st = 0, id = 0;
       if (lane == 0) {
@@ -863,15 +877,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (st == 1u) id = q_id[k];
       }
       st = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
-      if (st == 1u)
-        return ((pool_first * kStealSplit + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kUnit) | (c % kUnit);
+      if (st == 1u) return ((pool_first + (uint32_t)__builtin_amdgcn_readfirstlane((int)id)) * kRound) | (c % kRound);
       if (st == 2u) break;
-      if (wait_expired(spin, t0)) { // never in a healthy launch: fail loudly, do not hang
+      publish(); // never wait holding a claim
+      if (wait_spin(spin)) { // never in a healthy launch: fail loudly, do not hang
         if (lane == 0) report_err(kErrStealWait);
         break;
       }
-      publish(); // never wait holding a claim
-      __builtin_amdgcn_s_sleep(2);
     }
     more = false;
     return n_tasks;
@@ -1041,13 +1053,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     // DYN output: CRC of the task with counter index c into the LDS ring; the
     // wave completing a round stores the round's CRCs as one whole line.
-    // A pool round completes per unit (kUnit tasks: its own done count and
-    // store); its slot is freed once all kStealSplit units are stored.
     auto dyn_out = [&](uint32_t c, uint32_t tsk, uint32_t res) {
       const uint32_t rnd = c / kRound, idx = c % kRound, slot = rnd % kDynSlots;
-      const bool split = kStealSplit > 1 && steal && rnd >= steal_s; // a pool round: per-unit completion
-      const uint32_t usz = split ? kUnit : kRound, unit = split ? idx / kUnit : 0u;
-      uint32_t *done = s_ctl + 1 + slot * kStealSplit + unit, *gen = s_ctl + kGen, *ring = s_ctl + kRingBuf;
+      uint32_t *done = s_ctl + 1 + slot, *gen = s_ctl + kGen, *ring = s_ctl + kRingBuf;
       uint32_t old = 0;
       publish(); // the ring wait below must not hold a claim
       if (lane == 0) {
@@ -1057,11 +1065,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      // the unit's first global task (whole rounds and pool units are aligned)
-      const uint32_t base = tsk & ~(usz - 1u);
-      const uint32_t cnt = (n_tasks - base < usz) ? n_tasks - base : usz;
-      if (old + 1u == cnt) { // this wave completed the unit
-        const uint32_t v = ring[slot * kRound + unit * kUnit + (lane % usz)];
+      // the round's first global task (rounds are aligned)
+      const uint32_t base = tsk & ~(kRound - 1u);
+      const uint32_t cnt = (n_tasks - base < kRound) ? n_tasks - base : kRound;
+      if (old + 1u == cnt) { // this wave completed the round
+        const uint32_t v = ring[slot * kRound + (lane % kRound)];
         if constexpr ((ABL & kRowsAblNoStore) == 0) {
           if (lane < cnt) store_out(a.out + oidx(base + lane), v);
         } else {
@@ -1069,13 +1077,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         }
         if (lane == 0) {
           *done = 0;
-          bool last = true;
-          if (split) {
-            uint32_t *stored = s_ctl + kStored + slot;
-            last = __hip_atomic_fetch_add(stored, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1u == kStealSplit;
-            if (last) *stored = 0;
-          }
-          if (last) __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         j0 += cnt;
       }
@@ -1535,46 +1537,77 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // calls and four seed loads (C1: the QB = 4 rows were bound by the scalar
     // unit, PMC ~2.7x the SALU of a QB = 1 row).
     const bool affine = !RAGGED && (a.stride % 4u) == 0;
-    QuarterInfo aq[4];
     QuadMeta aqm;
-    bool afull = true;
     aqm.sl = 0;
+    // Uniform batches (round 4): ONE buffer descriptor per row, at B = the 16-B
+    // block holding body 4g's first byte.  Quarter b reads body 4g+b's window
+    // (the 1 KiB ending at the body's 16-B-rounded end) at offsets
+    // (p_b - B) - front_b + 16k, front_b = 1024 - len - z_b the window offset of
+    // the body's first byte; pieces wholly before the body get the out-of-range
+    // offset (zeros), exactly as with a descriptor per quarter (rounds 1-3: four
+    // descriptors, 16 SGPRs, and per-quarter 64-bit bases kept live -- the C1
+    // kernel spilled 31 SGPRs).  Affine batches (stride % 4 == 0, so 4 * stride
+    // keeps the 16-B phase): the offsets do not depend on g, one VGPR each.
+    uint32_t aoff[4] = {kOobOffset, kOobOffset, kOobOffset, kOobOffset};
     if constexpr (!RAGGED) {
+      const uint32_t ph = (uint32_t)(uintptr_t)a.base & 15u;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        aq[b].len = a.len;
-        aq[b].p0 = a.base + (uint64_t)b * a.stride;
-        aq[b].z = (uint32_t)(0u - (uint32_t)(uintptr_t)(aq[b].p0 + a.len)) & 15u;
-        aq[b].vstart = (int64_t)a.len + aq[b].z - (int64_t)kQuarter;
-        afull = afull && aq[b].vstart == 0 && a.len != 0;
-        aqm.lz[b] = (a.len << 4) | aq[b].z;
-        const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, a.len + aq[b].z);
+        const uint32_t z = (uint32_t)(0u - (uint32_t)((uintptr_t)a.base + (uint64_t)b * a.stride + a.len)) & 15u;
+        const uint32_t front = kQuarter - a.len - z; // window offset of the body's first byte
+        aoff[b] = (a.len == 0u || pofs + 16u <= front) ? kOobOffset : ph + (uint32_t)b * (uint32_t)a.stride + pofs - front;
+        aqm.lz[b] = (a.len << 4) | z;
+        const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, a.len + z);
         aqm.sl = (hi == (uint32_t)b) ? seed : aqm.sl;
       }
     }
     auto issue = [&](uint32_t g, bool ok, uint64_t safe, u32x4 (&buf)[4]) -> QuadMeta {
-      QuarterInfo qi[4];
       QuadMeta qm;
-      bool full = ok;
       qm.sl = 0;
-      if (affine && ok && 4 * g + 4 <= n) {
-        const uint64_t gofs = (uint64_t)g * 4u * a.stride;
+      if constexpr (!RAGGED) {
+        uint64_t B = safe;
+        uint32_t off[4] = {kOobOffset, kOobOffset, kOobOffset, kOobOffset};
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          qi[b] = aq[b];
-          qi[b].p0 = aq[b].p0 + gofs;
-        }
-        qm = aqm;
-        full = afull;
-      } else {
+        for (int b = 0; b < 4; ++b) qm.lz[b] = 0u;
+        if (ok) {
+          const uint64_t p0 = (uint64_t)(uintptr_t)a.base + (uint64_t)g * 4u * a.stride;
+          B = p0 & ~(uint64_t)15;
+          if (affine && 4 * g + 4 <= n) {
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          qi[b] = quarter(g, b);
-          full = full && qi[b].vstart == 0 && qi[b].len != 0;
-          qm.lz[b] = (qi[b].len << 4) | qi[b].z;
-          const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, qi[b].len + qi[b].z);
-          qm.sl = (hi == (uint32_t)b) ? seed : qm.sl;
+            for (int b = 0; b < 4; ++b) off[b] = aoff[b];
+            qm = aqm;
+          } else { // a last partial group, or a stride that moves the 16-B phase
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const bool live = 4 * g + b < n && a.len != 0u;
+              const uint32_t rel = (uint32_t)(p0 & 15u) + (uint32_t)b * (uint32_t)a.stride; // p_b - B
+              const uint32_t z = (uint32_t)(0u - (uint32_t)(p0 + (uint64_t)b * a.stride + a.len)) & 15u;
+              const uint32_t front = kQuarter - a.len - z;
+              off[b] = (!live || pofs + 16u <= front) ? kOobOffset : rel + pofs - front;
+              qm.lz[b] = live ? (a.len << 4) | z : 0u;
+              const uint32_t seed = (mode == kModeRaw || !live) ? 0u : ld_const(a.tq, a.len + z);
+              qm.sl = (hi == (uint32_t)b) ? seed : qm.sl;
+            }
+          }
         }
+        if constexpr ((ABL & kRowsAblNoLoad) != 0) {
+          synth(g, buf);
+        } else {
+          const __amdgpu_buffer_rsrc_t row = row_rsrc(B);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row, off[b]);
+        }
+        return qm;
+      }
+      QuarterInfo qi[4];
+      bool full = ok;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        qi[b] = quarter(g, b);
+        full = full && qi[b].vstart == 0 && qi[b].len != 0;
+        qm.lz[b] = (qi[b].len << 4) | qi[b].z;
+        const uint32_t seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, qi[b].len + qi[b].z);
+        qm.sl = (hi == (uint32_t)b) ? seed : qm.sl;
       }
       if constexpr ((ABL & kRowsAblNoLoad) != 0) {
         synth(g, buf);
@@ -1612,9 +1645,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     auto dyn_out4 = [&](uint32_t c, uint32_t tsk, const uint32_t (&v)[4]) {
       constexpr uint32_t kW = kRound * 4; // CRCs per round (64 or 128)
       const uint32_t rnd = (uint32_t)(c / kRound), idx = (uint32_t)(c % kRound), slot = rnd % kDynSlots;
-      const bool split = kStealSplit > 1 && steal && rnd >= steal_s; // a pool round: per-unit completion (QB = 1)
-      const uint32_t usz = split ? kUnit : kRound, unit = split ? idx / kUnit : 0u;
-      uint32_t *done = s_ctl + 1 + slot * kStealSplit + unit, *gen = s_ctl + kGen;
+      uint32_t *done = s_ctl + 1 + slot, *gen = s_ctl + kGen;
       uint32_t *ring = s_ctl + kRingBuf + slot * kW;
       uint32_t old = 0;
       publish(); // the ring wait below must not hold a claim
@@ -1625,28 +1656,21 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       old = (uint32_t)__builtin_amdgcn_readfirstlane((int)old);
-      // first group of the unit (whole rounds and pool units are aligned)
-      const uint32_t base = tsk & ~(usz - 1u);
-      const uint32_t cnt = (ngroups - base < usz) ? (uint32_t)(ngroups - base) : usz;
+      // first group of the round (rounds are aligned)
+      const uint32_t base = tsk & ~(kRound - 1u);
+      const uint32_t cnt = (ngroups - base < kRound) ? (uint32_t)(ngroups - base) : kRound;
       if (old + 1u == cnt) {
-        const uint32_t ibase = 4 * base, w = 4 * usz; // the unit's CRCs: 4 per group
-        const uint32_t nit = (n - ibase < w) ? (uint32_t)(n - ibase) : w;
-        const uint32_t *u = ring + unit * kUnit * 4;
-        const uint32_t v0 = u[lane % w];
+        const uint32_t ibase = 4 * base;
+        const uint32_t nit = (n - ibase < kW) ? (uint32_t)(n - ibase) : kW;
+        const uint32_t v0 = ring[lane];
         if (lane < nit) store_out(a.out + oidx(ibase + lane), v0);
-        if (w > 64) {
-          const uint32_t v1 = u[64 + lane]; // (w = 128)
+        if constexpr (kW > 64) {
+          const uint32_t v1 = ring[64 + lane];
           if (64 + lane < nit) store_out(a.out + oidx(ibase + 64 + lane), v1);
         }
         if (lane == 0) {
           *done = 0;
-          bool last = true;
-          if (split) {
-            uint32_t *stored = s_ctl + kStored + slot;
-            last = __hip_atomic_fetch_add(stored, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1u == kStealSplit;
-            if (last) *stored = 0;
-          }
-          if (last) __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         j0 += cnt;
       }

@@ -13,11 +13,12 @@
 // GPU caches -- sc0 sc1 loads / stores, no cache-wide fence):
 //   host   writes the body right-aligned into body[slot] (virtual buffer of
 //          64 * seg bytes, seg = 4 / 8 / 16 bytes per lane by length), then
-//          len[slot], then bumps seq[slot] (x86 stores stay in order);
-//   wave   polls the seq words of its kSvcPer slots (one load from one line,
-//          lane i = slot i); a seq it has not answered is a request: it reads len and the
-//          body (every lane its seg bytes), computes the CRC and stores
-//          {crc, seq} into res[slot] (one 64-bit store);
+//          req[slot] = {len, seq} as ONE 64-bit store (x86 stores stay in order);
+//   wave   polls the request words of its kSvcPer slots (one load, lane i =
+//          slot i); a seq it has not answered is a request: it reads the body
+//          (every lane its seg bytes; the loads of all its pending slots in
+//          flight together), computes the CRC and stores {crc, seq} into
+//          res[slot] (one 64-bit store);
 //   host   spins on res[slot] until the seq matches.
 // The waves share the time of the last request in LDS (4 bytes) and all leave
 // after idle_ticks without one, after the kernel's lifetime cap, or when the
@@ -58,38 +59,48 @@ __device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One request: body of len <= kSvcMaxLen bytes at V = body + 64*seg - len.
-template <uint32_t SEG>
-__device__ __forceinline__ uint32_t serve_crc0(const uint8_t *body, uint32_t len, uint32_t lane, uint32_t kshift) {
-  constexpr uint32_t kWords = SEG / 4;
-  const uint32_t off0 = 64u * SEG - len; // V offset of the body's first byte
-  uint32_t w[kWords];
-  if constexpr (SEG == 16) {
-    const uint4 v = ld_sys16(body, 64u * SEG, lane * 16u);
-    w[0] = v.x;
-    w[1] = v.y;
-    w[2] = v.z;
-    w[3] = v.w;
+// A request's body words: lane L's seg bytes of V = body + 64*seg - len..., as
+// dwords (the words past seg/4 are zero).  Issued for every pending slot of the
+// wave before any is computed, so their PCIe round trips overlap.
+struct Body {
+  uint32_t w[4];
+};
+__device__ __forceinline__ Body load_body(const uint8_t *body, uint32_t seg, uint32_t lane) {
+  Body b;
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(body + lane * seg);
+  if (seg == 16u) {
+    const uint4 v = ld_sys16(body, 64u * 16u, lane * 16u);
+    b.w[0] = v.x;
+    b.w[1] = v.y;
+    b.w[2] = v.z;
+    b.w[3] = v.w;
   } else {
-#pragma unroll
-    for (uint32_t d = 0; d < kWords; ++d) w[d] = ld_sys32(reinterpret_cast<const uint32_t *>(body + lane * SEG) + d);
+    b.w[0] = ld_sys32(p);
+    b.w[1] = seg == 8u ? ld_sys32(p + 1) : 0u;
+    b.w[2] = 0u;
+    b.w[3] = 0u;
   }
+  return b;
+}
+
+// crc0 of V: the lane's chain over its seg / 4 words (bytes before the body
+// masked), shifted to V's end by the lane's constant, XORed over the wave.
+__device__ __forceinline__ uint32_t body_crc0(const Body &b, uint32_t seg, uint32_t len, uint32_t lane,
+                                              uint32_t kshift) {
+  const uint32_t off0 = 64u * seg - len; // V offset of the body's first byte
   uint32_t s = 0;
 #pragma unroll
-  for (uint32_t d = 0; d < kWords; ++d) {
-    const uint32_t keep = svc::keep_mask(lane * SEG + 4 * d, off0);
-    s = svc::crc0_word(s ^ (w[d] & keep));
-  }
-  // shift to V's end, then XOR over the wave
+  for (uint32_t d = 0; d < 4; ++d)
+    if (4u * d < seg) s = svc::crc0_word(s ^ (b.w[d] & svc::keep_mask(lane * seg + 4u * d, off0)));
   s = svc::mulmod(s, kshift);
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) s ^= (uint32_t)__shfl_xor((int)s, m, 64);
   return s;
 }
 
-__global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void crc32_service_kernel(SvcShared *sh, const uint32_t *tq,
-                                                                       const uint32_t *kshift, uint64_t idle_ticks,
-                                                                       uint64_t life_ticks, uint32_t instance) {
+__global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void crc32_service_kernel(
+    SvcShared *sh, const uint32_t *tq, const uint32_t *kshift, uint64_t idle_ticks, uint64_t life_ticks,
+    uint32_t instance) {
   __shared__ uint32_t s_last;  // low 32 bits of the last request's s_memrealtime
   __shared__ uint32_t s_alive; // waves still in the loop
   const uint32_t lane = threadIdx.x & 63u;
@@ -102,32 +113,41 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
   __syncthreads();
   // per-lane constants: shift of this lane's segment to V's end, per seg class
   const uint32_t k4 = kshift[0 * 64 + lane], k8 = kshift[1 * 64 + lane], k16 = kshift[2 * 64 + lane];
-  const uint32_t slot0 = wave * kSvcPer;
-  // lane i < kSvcPer: the seq this wave last answered for slot slot0 + i
+  // wave w owns slots w + kSvcWaves * i (i < kSvcPer): the host hands slots out
+  // in index order, so concurrent callers land on different waves
+  const uint32_t myslot = wave + kSvcWaves * (lane < kSvcPer ? lane : 0u);
+  // lane i < kSvcPer: the seq this wave last answered for its slot i
   uint32_t served = 0;
-  if (lane < kSvcPer) served = (uint32_t)(__hip_atomic_load(&sh->res[slot0 + lane][0], __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+  if (lane < kSvcPer)
+    served = (uint32_t)(__hip_atomic_load(&sh->res[myslot][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
   for (uint32_t poll = 0;; ++poll) {
-    const uint32_t seq = (lane < kSvcPer) ? ld_sys32(&sh->seq[slot0 + lane]) : 0u;
+    // one 64-bit word per slot, {len, seq}: the host stores it whole, after the body
+    const uint64_t rq =
+        (lane < kSvcPer) ? __hip_atomic_load(&sh->req[myslot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    const uint32_t seq = (uint32_t)(rq >> 32);
     uint64_t pend = __builtin_amdgcn_ballot_w64(lane < kSvcPer && seq != served);
     if (pend != 0) {
-      while (pend != 0) {
-        const uint32_t i = (uint32_t)__builtin_ctzll(pend);
-        pend &= pend - 1;
-        const uint32_t slot = slot0 + i;
-        const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)seq, (int)i);
-        const uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sys32(&sh->len[slot]));
-        uint32_t c0 = 0;
-        const uint8_t *body = sh->body[slot];
-        const uint32_t seg = svc::seg_of(len);
-        if (seg == 4u) c0 = serve_crc0<4>(body, len, lane, k4);
-        else if (seg == 8u) c0 = serve_crc0<8>(body, len, lane, k8);
-        else c0 = serve_crc0<16>(body, len <= kSvcMaxLen ? len : kSvcMaxLen, lane, k16);
-        const uint32_t crc = len == 0u ? 0u : ~(tq[len <= kSvcMaxLen ? len : 0u] ^ c0);
+      // every pending slot's body loads first, then the CRCs
+      Body body[kSvcPer];
+      uint32_t lens[kSvcPer], seqs[kSvcPer];
+#pragma unroll
+      for (uint32_t i = 0; i < kSvcPer; ++i) {
+        const bool p = (pend >> i) & 1u;
+        lens[i] = p ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rq, (int)i) : 0u;
+        if (lens[i] > kSvcMaxLen) lens[i] = kSvcMaxLen; // (the host never sends more)
+        seqs[i] = (uint32_t)__builtin_amdgcn_readlane((int)seq, (int)i);
+        if (p) body[i] = load_body(sh->body[wave + kSvcWaves * i], svc::seg_of(lens[i]), lane);
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kSvcPer; ++i) {
+        if (!((pend >> i) & 1u)) continue;
+        const uint32_t len = lens[i], seg = svc::seg_of(len);
+        const uint32_t c0 = body_crc0(body[i], seg, len, lane, seg == 4u ? k4 : seg == 8u ? k8 : k16);
+        const uint32_t crc = len == 0u ? 0u : ~(tq[len] ^ c0);
         if (lane == 0)
-          __hip_atomic_store(&sh->res[slot][0], (uint64_t)crc | ((uint64_t)q << 32), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-        served = (lane == i) ? q : served;
+          __hip_atomic_store(&sh->res[wave + kSvcWaves * i][0], (uint64_t)crc | ((uint64_t)seqs[i] << 32),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        served = (lane == i) ? seqs[i] : served;
       }
       if (lane == 0)
         __hip_atomic_store(&s_last, (uint32_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,

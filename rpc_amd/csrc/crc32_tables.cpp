@@ -81,6 +81,14 @@ void build_scalar_tab(uint32_t *tab) {
     nibble_table(1u << k, reinterpret_cast<uint32_t(*)[16]>(tab + 1024 + (k - kScalarNibK0) * 128));
 }
 
+void build_lds_image_compact(const uint32_t *img, uint32_t *compact) {
+  const uint8_t *b = reinterpret_cast<const uint8_t *>(img);
+  for (uint32_t tbl = 0; tbl < 4; ++tbl)
+    for (uint32_t v = 0; v < 256; ++v) // copy 0 of table tbl, row v
+      memcpy(compact + tbl * 256 + v, b + (tbl >> 1) * kLdsMainRegion1 + v * 256 + (tbl & 1) * 128, 4);
+  memcpy(reinterpret_cast<uint8_t *>(compact) + kImgTailOfs, b + kLdsST1, kLdsBytesV3 - kLdsST1);
+}
+
 void build_tq(uint32_t *tq) {
   for (uint32_t q = 0; q < kTqEntries; ++q) tq[q] = gf2_shift_bytes(0xFFFFFFFFu, q);
 }

@@ -441,7 +441,7 @@ void init_device(int dev) {
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(dev);
   hipError_t e = hipSuccess;
-  e = (e == hipSuccess) ? hipMalloc(&c.img, kLdsBytesV3) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.img, kImgHbmBytes) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.big_dbl, kBigDblWords * 4) : e;
@@ -450,7 +450,13 @@ void init_device(int dev) {
   if (e == hipSuccess) *reinterpret_cast<volatile uint32_t *>(c.err) = 0;
   if (e == hipSuccess) {
     build_lds_image_v2(img.data());
-    e = hipMemcpy(c.img, img.data(), kLdsBytesV3, hipMemcpyHostToDevice);
+    if (kImgCompact) {
+      std::vector<uint32_t> compact(kImgCompactBytes / 4);
+      build_lds_image_compact(img.data(), compact.data());
+      e = hipMemcpy(c.img, compact.data(), kImgCompactBytes, hipMemcpyHostToDevice);
+    } else {
+      e = hipMemcpy(c.img, img.data(), kLdsBytesV3, hipMemcpyHostToDevice);
+    }
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);
@@ -683,6 +689,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     sl.p = sl.slot->p;
     sl.pool = c.steal;
     sl.s = s;
+    a.test_giveup = take_test_giveup(); // (the plain rows pass does not steal)
   }
   StealLease rsl; // RPCCRC_RAGGED_STEAL=1: the plain rows pass deals its tail from a steal counter too
   if (split) {
@@ -993,7 +1000,7 @@ void svc_init(DeviceCtx &c) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking);
   (void)hipSetDevice(prev);
   v->tq = c.tq;
-  for (int i = kSvcSlots - 1; i >= 0; --i) v->free_slots.push_back(i);
+  for (int i = kSvcSlots - 1; i >= 0; --i) v->free_slots.push_back(i); // slot 0 first: 8 callers on 8 waves
   v->ok = e == hipSuccess;
   if (v->ok) {
     std::lock_guard<std::mutex> g(g_services_mu);
@@ -1040,11 +1047,10 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
   SvcShared *sh = v.sh;
   const uint32_t seg = svc::seg_of(len);
   memcpy(sh->body[slot] + 64u * seg - len, src, len);
-  reinterpret_cast<volatile uint32_t *>(sh->len)[slot] = len;
   uint32_t q = ++v.seq[slot];
   if (q == 0) q = ++v.seq[slot]; // 0: the answered seq of a fresh slot
-  std::atomic_thread_fence(std::memory_order_release); // body and len before seq (x86: a compiler barrier)
-  reinterpret_cast<volatile uint32_t *>(sh->seq)[slot] = q;
+  std::atomic_thread_fence(std::memory_order_release); // the body before the request word (x86: a compiler barrier)
+  reinterpret_cast<volatile uint64_t *>(sh->req)[slot] = (uint64_t)len | ((uint64_t)q << 32);
   bool ok = svc_ensure(c, v);
   const volatile uint64_t *res = &sh->res[slot][0];
   uint64_t r = *res;

@@ -119,7 +119,9 @@ def test_error_words_per_call_and_clearable():
         rpc_crc32_device_status and from every later asynchronous call, until
         rpc_crc32_device_clear_status; synchronous calls keep working meanwhile.
     Forced in a child process on the fault-injection build librpccrc_test.so
-    (RPCCRC_TEST_STEAL_GIVEUP=2: the next two stealing launches give up)."""
+    (RPCCRC_TEST_STEAL_GIVEUP=2: the next two stealing launches give up).  (Round 4's
+    first version sent one 512 MiB body, whose 16 KiB chunks do not steal: the hook
+    then hit the clean call instead.)"""
     import os
     import subprocess
     import sys
@@ -128,10 +130,12 @@ import numpy as np, torch, rpc_amd
 from oracle import oracle
 torch.cuda.set_device(0)
 assert rpc_amd.device_status() == 0
-# (a) host batch, one 512 MiB body (> one 256 MiB stage: chunked, stealing) -> give-up #1
-big = oracle.splitmix_bytes(512 << 20, 0xB16E)
-want_big = oracle.crc32(big)
-offs, lens = np.array([0], np.uint64), np.array([512 << 20], np.uint32)
+# (a) host batch of 256 x 1 MiB bodies: one stage, every body on the big-body
+# route, whose chunk pass deals its tail from a steal pool -> give-up #1
+big = oracle.splitmix_bytes(256 << 20, 0xB16E)
+offs = np.arange(256, dtype=np.uint64) * np.uint64(1 << 20)
+lens = np.full(256, 1 << 20, dtype=np.uint32)
+want_big = oracle.crc32_batch(big, offs, lens)
 try:
     rpc_amd.crc32_batch(big, offs, lens)
     print("host1", 0)
@@ -152,7 +156,7 @@ except rpc_amd.RpcCrcError as e:
     print("next", e.code)
 # (c) synchronous calls are not affected by the device word
 print("dropin", rpc_amd.rpc_crc32(b"123456789") == 0xCBF43926)
-print("host2", int(rpc_amd.crc32_batch(big, offs, lens)[0]) == want_big)
+print("host2", bool(np.array_equal(rpc_amd.crc32_batch(big, offs, lens), want_big)))
 # (d) clear: asynchronous calls work again, every CRC exact
 print("clear", rpc_amd.device_clear_status(), rpc_amd.device_status())
 got = rpc_amd.device_uniform(base, n, L).cpu().numpy().view(np.uint32)

@@ -82,10 +82,6 @@ for s in $STEPS; do
     bench_c2) run bench_c2 600 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive ;;
     bench_c2_rows) run bench_c2_rows 600 python bench.py --config c2 --ragged-path rows --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
     timeline) run timeline 300 python tools/probe.py --mode timeline --reps 3 ;;
-    timeline_split) # per-wave timelines of C1 with whole-round (head) vs split pool claims
-           run timeline_c1_split1 300 python tools/probe.py --mode timeline --reps 3 --config c1 --steal &&
-           RPCCRC_PROBE_LIB=$PWD/abtest/libprobe_split2.so run timeline_c1_split2 300 python tools/probe.py --mode timeline --reps 3 --config c1 --steal &&
-           RPCCRC_PROBE_LIB=$PWD/abtest/libprobe_split4.so run timeline_c1_split4 300 python tools/probe.py --mode timeline --reps 3 --config c1 --steal ;;
     timeline_c1) run timeline_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 ;;
     timeline_steal) run timeline_steal_ns 300 python tools/probe.py --mode timeline --reps 3 --steal &&
                     run timeline_steal_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 --steal ;;

@@ -16,12 +16,14 @@ uint32_t *g_tq = nullptr;
 
 int ensure_tables() {
   if (g_img) return 0;
-  std::vector<uint32_t> img(kLdsBytesV3 / 4), tq(kTqEntries);
+  std::vector<uint32_t> img(kLdsBytesV3 / 4), compact(kImgCompactBytes / 4), tq(kTqEntries);
   build_lds_image_v2(img.data());
+  build_lds_image_compact(img.data(), compact.data());
   build_tq(tq.data());
-  if (hipMalloc(&g_img, kLdsBytesV3) != hipSuccess) return -1;
+  if (hipMalloc(&g_img, kImgHbmBytes) != hipSuccess) return -1;
   if (hipMalloc(&g_tq, kTqEntries * 4) != hipSuccess) return -1;
-  if (hipMemcpy(g_img, img.data(), kLdsBytesV3, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (hipMemcpy(g_img, kImgCompact ? compact.data() : img.data(), kImgHbmBytes, hipMemcpyHostToDevice) != hipSuccess)
+    return -1;
   if (hipMemcpy(g_tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice) != hipSuccess) return -1;
   return 0;
 }
