@@ -20,7 +20,7 @@ except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("RPCCRC_LIB", os.path.join(HERE, "lib", "librpccrc.so"))
+LIB_PATH = os.environ.get("RPCCRC_LIB") or os.path.join(HERE, "lib", "librpccrc.so")  # (empty = in-tree)
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -45,7 +45,7 @@ def _sig(name, restype, *argtypes):
         # A/B runs may point RPCCRC_LIB at an older build (tools/ab_lib.sh) that
         # lacks a newer entry point; the in-tree library must export them all
         # (tests/test_abi.py).
-        if "RPCCRC_LIB" in os.environ:
+        if os.environ.get("RPCCRC_LIB"):
             return None
         raise
     f.restype = restype

@@ -135,7 +135,10 @@ constexpr uint32_t kSvcSlots = kSvcWaves * kSvcPer;    // concurrent drop-in cal
 constexpr uint32_t kSvcMaxLen = 1024;                  // MAX_BODY_LEN (rpc.h:17)
 constexpr uint32_t kSvcStop = 0, kSvcExited = 1;       // SvcShared::ctl words
 struct SvcShared {
-  uint64_t req[kSvcSlots];            // host: {len (low), seq (high)} of each slot, one store, after the body
+  // host: {len (low), seq (high)} of each slot, one store after the body; one
+  // 64-B line per slot (a shared line was written by up to 8 caller threads
+  // while 8 waves polled it: 10 callers took 30 us a call, r04c)
+  uint64_t req[kSvcSlots][8];
   uint64_t res[kSvcSlots][8];         // device: {crc, seq} (crc in the low half), one 64-B line per slot
   uint32_t ctl[16];                   // [kSvcStop] host: leave now; [kSvcExited] device: last instance that left
   uint8_t body[kSvcSlots][kSvcMaxLen]; // host: the body, right-aligned in 64 * seg bytes (seg 4 / 8 / 16)

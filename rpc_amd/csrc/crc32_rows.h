@@ -412,6 +412,21 @@ constexpr bool kSubRows = RPCCRC_SUBROWS != 0;
 #define RPCCRC_LANE_HORNER 1
 #endif
 constexpr bool kLaneHorner = RPCCRC_LANE_HORNER != 0;
+// Ragged QB = 1: an item's offset and length loads issued together, then one
+// wait (round 4).  The compiler had sunk the offset load below the length's
+// route test: two serial scalar-load round trips per item (ISA).
+#ifndef RPCCRC_META_COISSUE
+#define RPCCRC_META_COISSUE 1
+#endif
+constexpr bool kMetaCoissue = RPCCRC_META_COISSUE != 0;
+// Ragged QB = 1: zlib seeds from the LDS image (TQ16 + a distributed ZI step)
+// instead of a scalar load of Tq[hd] per item.  Any scalar load in flight makes
+// the chain's next LDS wait an lgkmcnt(0) (SMEM returns out of order), so the
+// seed load issued with the next item's metadata stalled the current row's
+// chain.
+#ifndef RPCCRC_LDS_SEED
+#define RPCCRC_LDS_SEED 0
+#endif
 
 namespace rows {
 
@@ -668,6 +683,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   constexpr uint32_t kRound = dyn_round(QB); // tasks per dealing round
   constexpr uint32_t kDynSlots = dyn_slots(QB);
   constexpr uint32_t kGen = dyn_gen_ofs(QB), kRingBuf = dyn_ringbuf_ofs(QB);
+  constexpr bool kLdsSeed = (ABL & kRowsAblLdsSeed) != 0 || (RPCCRC_LDS_SEED != 0 && QB == 1 && RAGGED);
   // sub-row first rows: ragged QB = 1 with the plain chain (image V3 adds SQ)
   constexpr bool kSub = kSubRows && QB == 1 && RAGGED && !kTwoChains &&
                         (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblHalfChain | kRowsAblNoSub)) == 0;
@@ -977,8 +993,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // 0 can start before the item (when hd < 4096).
     auto meta = [&](uint32_t item, uint64_t &p0, uint32_t &hd, uint32_t &len, uint32_t &z, uint32_t &nr,
                     uint32_t &seed) {
-      const uint64_t off = RAGGED ? ld_const(a.offsets, item) : (uint64_t)item * a.stride;
+      uint64_t off = RAGGED ? ld_const(a.offsets, item) : (uint64_t)item * a.stride;
       len = RAGGED ? ld_const(a.lengths, item) : a.len;
+      if constexpr (RAGGED && kMetaCoissue) __asm__ volatile("" : "+s"(off), "+s"(len)); // both loads, one wait
       if constexpr (RAGGED) {
         // a routed big body is empty here (launch_big_route computes it)
         if (len >= a.big_min && a.routed != nullptr) {
@@ -998,8 +1015,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         nr = 1u;
         hd = 0u;
       }
-      if constexpr ((ABL & kRowsAblLdsSeed) != 0)
-        seed = hd; // resolved in compute
+      if constexpr (kLdsSeed)
+        seed = hd; // resolved in compute / lane_horner_p
       else
         seed = (mode == kModeRaw) ? 0u : ld_const(a.tq, hd);
     };
@@ -1101,7 +1118,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
                       uint32_t tsk, RowMerge m) {
       const bool last = r + 1 == nr;
       // Horner over rows: A_4096(W), or the zlib seed on the item's first row.
-      if constexpr ((ABL & kRowsAblLdsSeed) != 0) {
+      if constexpr (kLdsSeed) {
         if (r == 0) {
           const uint32_t first = seed, up = (first + 15u) & ~15u;
           uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
@@ -1269,6 +1286,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       if (r != 0) {
         lacc = rw_map(lds, lacc) ^ chain;
       } else { // a body's first row starts the accumulator (zlib's seed in lane 63)
+        if constexpr (kLdsSeed) { // seed holds hd: A_hd(F) = ZI_{up - hd}(TQ16[up / 16])
+          const uint32_t up = (seed + 15u) & ~15u;
+          uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
+          if (up != seed) w = dist_uniform(lds, w, kLdsZI2 + (up - seed - 1u) * 512u, dl);
+          seed = (mode == kModeRaw) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
+        }
         lacc = chain ^ ((lane == 63u) ? seed : 0u);
       }
       if (r + 1 == nr) {

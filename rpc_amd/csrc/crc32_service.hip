@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
   for (uint32_t poll = 0;; ++poll) {
     // one 64-bit word per slot, {len, seq}: the host stores it whole, after the body
     const uint64_t rq =
-        (lane < kSvcPer) ? __hip_atomic_load(&sh->req[myslot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+        (lane < kSvcPer) ? __hip_atomic_load(&sh->req[myslot][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
     const uint32_t seq = (uint32_t)(rq >> 32);
     uint64_t pend = __builtin_amdgcn_ballot_w64(lane < kSvcPer && seq != served);
     if (pend != 0) {

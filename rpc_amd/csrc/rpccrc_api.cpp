@@ -1050,7 +1050,7 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
   uint32_t q = ++v.seq[slot];
   if (q == 0) q = ++v.seq[slot]; // 0: the answered seq of a fresh slot
   std::atomic_thread_fence(std::memory_order_release); // the body before the request word (x86: a compiler barrier)
-  reinterpret_cast<volatile uint64_t *>(sh->req)[slot] = (uint64_t)len | ((uint64_t)q << 32);
+  *reinterpret_cast<volatile uint64_t *>(&sh->req[slot][0]) = (uint64_t)len | ((uint64_t)q << 32);
   bool ok = svc_ensure(c, v);
   const volatile uint64_t *res = &sh->res[slot][0];
   uint64_t r = *res;

@@ -68,6 +68,13 @@ for s in $STEPS; do
                RPCCRC_BIG_ALIGNED=$1 RPCCRC_BIG_CHUNK=$2 run frames_a$1_c$2_$i 300 python tools/frames_lifted.py 2 || exit 1
              done
            done ;;
+    frames_libs) # lifted-cap frames probe per library (A/B): FRAMES_LIBS="head name ..."
+           for i in 1 2; do
+             for l in ${FRAMES_LIBS:-head}; do
+               if [ "$l" = head ]; then lib=""; else lib=$PWD/abtest/$l.so; fi
+               RPCCRC_LIB=$lib run frames_${l}_$i 300 python tools/frames_lifted.py 2 || exit 1
+             done
+           done ;;
     prof_frames) run prof_frames 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_frames" -o run --output-format csv -- \
                    python3 tools/frames_lifted.py 3 ;;
     ragged) run ragged_${RAGGED_CFG:-c2} 300 python tools/probe.py --mode ragged --config ${RAGGED_CFG:-c2} --rounds ${RAGGED_ROUNDS:-3} --reps 5 ;;
