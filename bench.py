@@ -401,13 +401,15 @@ def frames_lifted_probe(device, n=1024, reps=5, seed=0x5EED0007):
     buf[pos] ^= 0x5A
     flagged = bool(v2[big] == rpc_amd.FRAME_BAD_CRC and (np.delete(v2, big) == rpc_amd.FRAME_OK).all())
     body = int(lens.sum())
+    aligned_4k = buf.data_ptr() % 4096 == 0  # span mode needs a 4 KiB-aligned stream
     del buf
     return {"frames": n, "bodies": "log-uniform 1 B - 64 MiB (LIFT_CAP)", "body_bytes": body,
             "routed_bodies_ge_256KiB": int((lens >= (256 << 10)).sum()),
             "verify_us": round(t_verify * 1e6, 1), "verify_GiBps": round(body / t_verify / GiB, 1),
             "verify_frames_per_s": round(n / t_verify, 1),
             "stamp_us": round(t_stamp * 1e6, 1), "stamp_GiBps": round(body / t_stamp / GiB, 1),
-            "all_stamped": stamped, "all_ok_after_stamp": all_ok, "corrupted_frame_flagged": flagged}
+            "all_stamped": stamped, "all_ok_after_stamp": all_ok, "corrupted_frame_flagged": flagged,
+            "route_span_mode": aligned_4k and os.environ.get("RPCCRC_BIG_SPAN", "1") != "0"}
 
 
 def stream_read_probe(w: Workload, reps=10):

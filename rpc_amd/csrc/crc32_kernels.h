@@ -80,7 +80,8 @@ constexpr uint64_t kBigMinChunk = 8192 - 16;       // end-aligned chunks (BigRou
 constexpr uint64_t kBigMinChunkAligned = 8192;     // address-aligned chunks (the default)
 struct BigRoute {
   uint32_t *routed;  // bit i: body i takes the route (ceil(n / 64) * 2 words, all written)
-  uint64_t *meta;    // [0] bodies claimed, [1] their bytes, [2] chunks, [3] chunk bytes
+  uint64_t *meta;    // [0] bodies claimed, [1] their bytes, [2] chunks, [3] chunk bytes,
+                     // [4] span rows, [5] span mode on (route-all span mode, below)
   uint32_t *b_idx;   // kBigMaxBodies: batch index of each routed body
   uint64_t *b_first; // kBigMaxBodies + 1: first chunk of each routed body
   uint64_t *c_off;   // kBigMaxChunks: chunk offsets / lengths / crc0
@@ -96,11 +97,20 @@ struct BigRoute {
   // no plain rows pass); the plan sums the lengths itself.
   uint32_t all_n = 0;
   const uint32_t *tq = nullptr;  // Tq[q] = A_q(0xFFFFFFFF): the combine seeds chunk 0 with it
+  // Span mode (route-all only; span_rows_max > 0, the batch base 4 KiB-aligned):
+  // when the plan finds the bodies dense in [base, base + 4096 * span_rows_max)
+  // (meta[5] = 1), the UNIFORM rows pass CRCs every whole 4 KiB block below the
+  // last body end into blk[] (meta[4] blocks), the ragged chunk pass has no
+  // chunks, and the fold takes a body's interior blocks from blk[] and its
+  // first / last partial block from the bytes themselves.
+  uint32_t *blk = nullptr;
+  uint64_t span_rows_max = 0;
   const uint32_t *dbl = nullptr; // kBigDblWords: the fold's doubling maps per chunk class (build_big_dbl)
 };
 // (The fold's doubling maps per chunk class: crc32_layout.h build_big_dbl.)
-size_t big_route_workspace_bytes(uint64_t n);
-BigRoute big_route_carve(void *ws, uint64_t n);
+// span_rows: the span pass's block table (span mode, 0: off)
+size_t big_route_workspace_bytes(uint64_t n, uint64_t span_rows = 0);
+BigRoute big_route_carve(void *ws, uint64_t n, uint64_t span_rows = 0);
 // Before the rows pass: flags and lists the big bodies (route.routed goes into
 // the rows pass's ItemsArgs).  Stream-ordered, no host round trip.
 // big_min: bodies of at least this many bytes are routed (kBigMin by default).
@@ -111,9 +121,17 @@ hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big
 // steal: a leased zeroed two-word counter for the chunk pass's tail stealing
 // (nullptr: static rounds); its event is recorded as the chunk pass's
 // completion (steal_done, *steal_recorded) like launch_rows.
+// span: the span pass's steal counter and event (span mode only).
+struct StealArgs {
+  uint32_t *p = nullptr;
+  hipEvent_t done = nullptr;
+  bool *recorded = nullptr;
+};
 hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,
                             hipStream_t s, uint32_t *steal = nullptr, hipEvent_t steal_done = nullptr,
-                            bool *steal_recorded = nullptr);
+                            bool *steal_recorded = nullptr, StealArgs span = StealArgs());
+// Most 4 KiB blocks of a span-mode route (16 GiB of stream per call).
+constexpr uint64_t kSpanMaxRows = 1ull << 22;
 
 constexpr uint32_t kShiftNibWords = 64u * 8u * 16u; // 32 KiB: the chunk combine's shift maps
 

@@ -774,6 +774,45 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
   } else {
     bytes = r.meta[1];
   }
+  if (r.span_rows_max != 0) { // span mode (route-all, base 4 KiB-aligned; BigRoute)
+    // The last body end, and the bytes of the whole blocks inside bodies (the
+    // blocks the fold takes from the span pass).  Dense: the span pass reads at
+    // most 1/16 more than those blocks (+ 1 MiB).
+    unsigned long long hi = 0, inner = 0;
+    for (uint64_t b = t; b < nb; b += 1024) {
+      const uint64_t s0 = offsets[b], L = lengths[b];
+      if (L == 0) continue;
+      const uint64_t e = s0 + L, j0 = s0 >> 12, j1 = (e - 1) >> 12;
+      hi = e > hi ? e : hi;
+      inner += (j1 > j0 + 1) ? (j1 - j0 - 1) << 12 : 0ull;
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+      const unsigned long long h = __shfl_xor(hi, m, 64);
+      hi = h > hi ? h : hi;
+      inner += __shfl_xor(inner, m, 64);
+    }
+    if (lane == 0) wsum[w] = inner;
+    __syncthreads();
+    unsigned long long inner_all = 0;
+    for (uint32_t k = 0; k < 16; ++k) inner_all += wsum[k];
+    __syncthreads();
+    if (lane == 0) wsum[w] = hi;
+    __syncthreads();
+    unsigned long long hi_all = 0;
+    for (uint32_t k = 0; k < 16; ++k) hi_all = wsum[k] > hi_all ? wsum[k] : hi_all;
+    __syncthreads();
+    const uint64_t rows = hi_all >> 12;
+    const bool dense = rows <= r.span_rows_max && (rows << 12) <= inner_all + inner_all / 16 + (1ull << 20);
+    if (t == 0) {
+      r.meta[4] = dense ? rows : 0;
+      r.meta[5] = dense ? 1 : 0;
+      if (dense) {
+        r.meta[2] = 0; // no chunks for the ragged chunk pass
+        r.meta[3] = 4096;
+      }
+    }
+    if (dense) return;
+  }
   // sum over bodies of (L / C + 2) bounds the chunks
   uint64_t chunk = r.min_chunk;
   while (bytes / chunk + 2 * nb > kBigMaxChunks) chunk <<= 1;
@@ -811,7 +850,7 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
 
 __global__ void __launch_bounds__(256) big_expand_aligned_kernel(const uint8_t *base, const uint64_t *offsets,
                                                                  const uint32_t *lengths, BigRoute r) {
-  const uint64_t nb = big_count(r), chunk = r.meta[3];
+  const uint64_t nb = (r.span_rows_max != 0 && r.meta[5] != 0) ? 0 : big_count(r), chunk = r.meta[3];
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint32_t i = big_body(r, b);
@@ -826,6 +865,47 @@ __global__ void __launch_bounds__(256) big_expand_aligned_kernel(const uint8_t *
   }
 }
 
+// ---- span mode (BigRoute.span_rows_max; route-all batches) --------------------
+// A body [s, e) (offsets from the 4 KiB-aligned base) covers blocks j0..j1: its
+// chunks are the aligned chunks of C = 4096 -- the first and last partial
+// blocks, whose crc0 the fold computes here from the bytes, and the interior
+// blocks j0 < j < j1, whose crc0 the span pass (uniform rows, RAW) left in blk[j].
+//
+// crc0 of a piece [ps, pe) of <= 4096 bytes, right-aligned in a 4096-byte
+// window (leading zeros leave crc0 unchanged): thread t's term is
+// A_4(dword of window bytes [4t, 4t + 4)), the bytes before ps masked; the
+// window's crc0 is XOR_t A_{4 (1023 - t)}(term_t) (span_fold_terms + the
+// workgroup step).  The dword comes from two aligned loads through a buffer
+// resource starting at ps & ~3 (offsets before it wrap and read 0; none lies
+// past the dword holding byte pe - 1) and v_alignbyte.
+__device__ __forceinline__ uint32_t span_piece_term(const uint8_t *base, uint64_t ps, uint64_t pe, uint32_t t,
+                                                    const uint32_t *a4) {
+  const uint64_t B = ps & ~3ull;
+  const uint32_t span = (uint32_t)(pe - B); // <= 4099
+  const uint32_t r = (uint32_t)pe & 3u;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base + B), (short)0,
+                                                                      (int)((span + 3u) & ~3u), 0x00020000);
+  const uint32_t a = span - 4096u + 4u * t - r; // aligned: window byte 4t lies at a + r
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)a, 0, 0);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a + 4u), 0, 0);
+  const uint32_t wd = __builtin_amdgcn_alignbyte(hi, lo, r);
+  const int d = (int)(4096u - (uint32_t)(pe - ps)) - (int)(4u * t); // bytes of this dword before ps
+  const uint32_t keep = d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d)));
+  return nib_map(a4, wd & keep);
+}
+// In-wave step: lanes hold crc0 of consecutive dwords; after the level of
+// distance d a lane holds its 2d-dword group's crc0 (the left half shifted
+// past the right half's 4d bytes by NIB[log2 4d]).
+__device__ __forceinline__ uint32_t span_fold_terms(uint32_t v, uint32_t lane, const uint32_t *nib) {
+#pragma unroll
+  for (uint32_t d = 1, k = 2; d < 64; d <<= 1, ++k) {
+    const uint32_t sh = nib_map(nib + 128u * k, v);
+    const uint32_t mine = (lane & d) ? v : sh;
+    v = mine ^ (uint32_t)__shfl_xor((int)mine, (int)d, 64);
+  }
+  return v;
+}
+
 // Block b folds routed bodies b, b + grid, ...: thread t runs Horner over
 // chunks t, t + 1024, ... of the first nch - 1 with the step map A_{1024 C},
 // shifts its partial by A_{j C} (j < 1024 chunks after its last one), and the
@@ -835,10 +915,11 @@ __global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t
                                                                    const uint32_t *lengths, BigRoute r,
                                                                    const uint4 *shift_nib, uint32_t *out) {
   __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
-  __shared__ uint32_t part[16];
+  __shared__ uint32_t part[16], part2[16], praw[2];
   const uint64_t nb = big_count(r);
   if (blockIdx.x >= nb) return;
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const bool span = r.span_rows_max != 0 && r.meta[5] != 0; // (span mode: chunk = 4096)
   const uint64_t chunk = r.meta[3];
   const uint32_t lc = (uint32_t)__builtin_ctzll(chunk);
   {
@@ -853,7 +934,71 @@ __global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t
   };
   const uint32_t *stepnib = nib + 128u * (lc + 10u); // A_{1024 C}
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
-  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+  for (uint64_t b = blockIdx.x; span && b < nb; b += gridDim.x) { // span mode (block-uniform)
+    const uint32_t i = (uint32_t)b; // route-all: body b
+    const uint64_t s = offsets[i], L = lengths[i], e = s + L;
+    const uint64_t j0 = s >> 12, j1 = L ? (e - 1) >> 12 : j0, nch = L ? j1 - j0 + 1 : 0;
+    // the first and last partial blocks' crc0 (one piece: the body lies in one block)
+    uint32_t v0 = 0, v1 = 0;
+    if (L) {
+      v0 = span_piece_term(base, s, nch == 1 ? e : (j0 + 1) << 12, t, nib + 128u * 2u);
+      if (nch > 1) v1 = span_piece_term(base, j1 << 12, e, t, nib + 128u * 2u);
+    }
+    v0 = span_fold_terms(v0, lane, nib);
+    v1 = span_fold_terms(v1, lane, nib);
+    if (lane == 0) {
+      part[w] = v0;
+      part2[w] = v1;
+    }
+    __syncthreads();
+    if (t == 0) { // the 16 waves' 256-B groups, A_256 = NIB[8]
+      uint32_t h = 0, g = 0;
+      for (uint32_t k = 0; k < 16; ++k) {
+        h = nib_map(nib + 128u * 8u, h) ^ part[k];
+        g = nib_map(nib + 128u * 8u, g) ^ part2[k];
+      }
+      praw[0] = h;
+      praw[1] = g;
+    }
+    __syncthreads();
+    const uint32_t head = praw[0], tail = praw[1];
+    uint32_t seed = 0; // A_{len0}(F): zlib's pre-conditioning enters with the first piece
+    if (t == 0 && nch != 0) {
+      const uint64_t len0 = (nch == 1 ? e : (j0 + 1) << 12) - s;
+      seed = apply(len0 & ~4095ull, r.tq[len0 & 4095u]);
+    }
+    const uint64_t m = nch ? nch - 1 : 0; // chunks folded into G: the head, then blocks j0 + 1 ..
+    uint32_t acc = 0;
+    constexpr uint32_t kB = 8;
+    for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * 1024u) {
+      uint32_t rv[kB];
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) {
+        const uint64_t k = k0 + q * 1024u;
+        rv[q] = k == 0 ? head : (k < m ? r.blk[j0 + k] : 0u);
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q)
+        if (k0 + q * 1024u < m) acc = nib_map(stepnib, acc) ^ rv[q] ^ (k0 + q == 0 ? seed : 0u);
+    }
+    if (t < m) {
+      for (uint32_t j = (uint32_t)((m - 1 - t) % 1024u); j; j &= j - 1)
+        acc = nib_map(nib + 128u * (lc + (uint32_t)__builtin_ctz(j)), acc);
+    }
+    for (int d = 1; d < 64; d <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, d, 64);
+    __syncthreads(); // (part[] was read above)
+    if (lane == 0) part[w] = acc;
+    __syncthreads();
+    if (t == 0) {
+      for (uint32_t k = 1; k < 16; ++k) acc ^= part[k];
+      uint32_t crc = 0;
+      if (nch == 1) crc = ~(head ^ seed);
+      else if (nch > 1) crc = ~(apply(e - (j1 << 12), acc) ^ tail);
+      out[i] = crc; // an empty body: crc32 = 0
+    }
+    __syncthreads();
+  }
+  for (uint64_t b = blockIdx.x; !span && b < nb; b += gridDim.x) {
     const uint32_t i = big_body(r, b);
     const uint64_t s = b0 + offsets[i], L = lengths[i], first = r.b_first[b], nch = r.b_first[b + 1] - first;
     const uint64_t e = s + L;
@@ -899,12 +1044,13 @@ __global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t
 
 } // namespace
 
-size_t big_route_workspace_bytes(uint64_t n) {
-  return align256((n + 63) / 64 * 8) + align256(32) + align256(kBigMaxBodies * 4) +
-         align256((kBigMaxBodies + 1) * 8) + align256(kBigMaxChunks * 8) + 2 * align256(kBigMaxChunks * 4);
+size_t big_route_workspace_bytes(uint64_t n, uint64_t span_rows) {
+  return align256((n + 63) / 64 * 8) + align256(64) + align256(kBigMaxBodies * 4) +
+         align256((kBigMaxBodies + 1) * 8) + align256(kBigMaxChunks * 8) + 2 * align256(kBigMaxChunks * 4) +
+         align256(span_rows * 4);
 }
 
-BigRoute big_route_carve(void *ws, uint64_t n) {
+BigRoute big_route_carve(void *ws, uint64_t n, uint64_t span_rows) {
   uint8_t *w = static_cast<uint8_t *>(ws);
   auto take = [&](size_t bytes) {
     uint8_t *p = w;
@@ -913,12 +1059,16 @@ BigRoute big_route_carve(void *ws, uint64_t n) {
   };
   BigRoute r;
   r.routed = reinterpret_cast<uint32_t *>(take((n + 63) / 64 * 8));
-  r.meta = reinterpret_cast<uint64_t *>(take(32));
+  r.meta = reinterpret_cast<uint64_t *>(take(64));
   r.b_idx = reinterpret_cast<uint32_t *>(take(kBigMaxBodies * 4));
   r.b_first = reinterpret_cast<uint64_t *>(take((kBigMaxBodies + 1) * 8));
   r.c_off = reinterpret_cast<uint64_t *>(take(kBigMaxChunks * 8));
   r.c_len = reinterpret_cast<uint32_t *>(take(kBigMaxChunks * 4));
   r.c_raw = reinterpret_cast<uint32_t *>(take(kBigMaxChunks * 4));
+  if (span_rows) {
+    r.blk = reinterpret_cast<uint32_t *>(take(span_rows * 4));
+    r.span_rows_max = span_rows;
+  }
   return r;
 }
 
@@ -933,9 +1083,14 @@ hipError_t launch_big_classify(const uint32_t *lengths, uint64_t n, uint32_t big
 }
 
 hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uint4 *shift_nib, bool nt, int max_blocks,
-                            hipStream_t s, uint32_t *steal, hipEvent_t steal_done, bool *steal_recorded) {
+                            hipStream_t s, uint32_t *steal, hipEvent_t steal_done, bool *steal_recorded,
+                            StealArgs span) {
   if (proto.n_items == 0) return hipSuccess;
   if (proto.mode != kModeFinal || proto.offsets == nullptr || proto.lengths == nullptr || !r.tq) return hipErrorInvalidValue;
+  // span mode: route-all over a 4 KiB-aligned base, aligned chunks, a block table
+  if (r.span_rows_max != 0 && (!r.all_n || !r.aligned || !r.blk || ((uintptr_t)proto.base & 4095u) != 0 ||
+                               r.span_rows_max > kSpanMaxRows))
+    return hipErrorInvalidValue;
   hipError_t e;
   if (r.aligned) {
     // address-aligned power-of-two chunks (>= 4 KiB; the fold's step map is
@@ -975,6 +1130,25 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
   a.steal = steal;
   e = launch_rows(a, 1, nt, max_blocks, s, steal_done, steal_recorded);
   if (e != hipSuccess) return e;
+  if (r.span_rows_max != 0) {
+    // the span pass: every whole 4 KiB block below the last body end, uniform
+    // rows (RAW), count on the device (0 unless the plan chose span mode)
+    ItemsArgs u = proto;
+    u.offsets = nullptr;
+    u.lengths = nullptr;
+    u.n_items = r.span_rows_max;
+    u.stride = 4096;
+    u.len = 4096;
+    u.n_dev = r.meta + 4;
+    u.out_idx = nullptr;
+    u.routed = nullptr;
+    u.big_min = 0xFFFFFFFFu;
+    u.mode = kModeRaw;
+    u.out = r.blk;
+    u.steal = span.p;
+    e = launch_rows(u, 1, nt, max_blocks, s, span.done, span.recorded);
+    if (e != hipSuccess) return e;
+  }
   // 1024 blocks (blocks past the routed-body count leave at once): a block folds
   // one body at a time, so the count bounds the serial bodies per block.
   if (r.aligned)

@@ -398,6 +398,13 @@ const uint64_t g_big_chunk = [] {
 constexpr uint32_t kRowsGroupShift = 0;           // rows kernel group dealing, G = 2^shift
 constexpr uint64_t kSplitMinFrames = 16384;       // fewer frames: one wave per body (rows kernel)
 constexpr uint64_t kRouteAllMax = 2048;           // lifted-cap frames batches up to this size: route-all
+// Route-all span mode (BigRoute): on by default; RPCCRC_BIG_SPAN=0
+// keeps every body on the chunk route.  Streams below kSpanMinBytes keep it too.
+const bool g_big_span = [] {
+  const char *e = getenv("RPCCRC_BIG_SPAN");
+  return !(e && e[0] == '0');
+}();
+constexpr uint64_t kSpanMinBytes = 1ull << 20;
 constexpr bool kAutoSplitFrames = true;           // AUTO frames batches: split (true) or packed (false)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
 // Chunks per packed slice, at least: a slice switch costs the wave two scalar
@@ -618,8 +625,11 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
 //  * route: bodies of >= kBigMin bytes go through the big-body chunk route
 //    (classify before, chunks + fold after) so a long body
 //    does not stream through a single wave.  Not with the packed kernel.
+//  * span_bytes (frames calls: the stream length; 0 otherwise): a route-all
+//    batch over a 4 KiB-aligned base may take the route's span mode (BigRoute).
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-           uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route, uint32_t *err = nullptr) {
+           uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route, uint32_t *err = nullptr,
+           uint64_t span_bytes = 0) {
   const int path = g_ragged_path.load(std::memory_order_relaxed);
   const bool nt = nontemporal();
   const int mb = max_blocks_for(c);
@@ -658,12 +668,6 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   size_t split_bytes = 0;
   if (split) RPCCRC_TRY(split_workspace_bytes(n, &split_bytes));
   split_bytes = (split_bytes + 255) & ~(size_t)255;
-  const size_t route_bytes = route ? big_route_workspace_bytes(n) : 0;
-  Lease ws;
-  if (split_bytes + route_bytes > 0)
-    if (const int rc = ws.get(c.ws, split_bytes + route_bytes, s)) return rc;
-  BigRoute r{};
-  StealLease sl; // the route's chunk pass deals its tail from this counter (device-counted)
   // Route-all: a lifted-cap frames batch of at most kRouteAllMax frames sends
   // every body through the chunk route (no classify pass and no plain rows
   // pass, whose longest non-routed body -- up to the 16 KiB small-batch
@@ -671,8 +675,21 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   // Bounded because the fold spends a block-wide reduction per body (1024
   // blocks): a few bodies per block cost less than the passes they replace.
   const bool route_all = route && small_bodies && !split && n <= kRouteAllMax && !g_big_min_env;
+  // Span mode (route-all over a 4 KiB-aligned stream of >= kSpanMinBytes; the
+  // plan still falls back to chunks when the bodies are sparse in it).
+  const uint64_t span_rows = (route_all && g_big_span && g_big_aligned && ((uintptr_t)base & 4095u) == 0 &&
+                              span_bytes >= kSpanMinBytes && (span_bytes >> 12) <= kSpanMaxRows)
+                                 ? span_bytes >> 12
+                                 : 0;
+  const size_t route_bytes = route ? big_route_workspace_bytes(n, span_rows) : 0;
+  Lease ws;
+  if (split_bytes + route_bytes > 0)
+    if (const int rc = ws.get(c.ws, split_bytes + route_bytes, s)) return rc;
+  BigRoute r{};
+  StealLease sl;  // the route's chunk pass deals its tail from this counter (device-counted)
+  StealLease ssl; // ... and its span pass from this one
   if (route) {
-    r = big_route_carve(ws.ptr() + split_bytes, n);
+    r = big_route_carve(ws.ptr() + split_bytes, n, span_rows);
     r.min_chunk = g_big_chunk;
     r.aligned = g_big_aligned;
     r.tq = c.tq;
@@ -689,6 +706,8 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     sl.p = sl.slot->p;
     sl.pool = c.steal;
     sl.s = s;
+    if (span_rows)
+      if (const int rc = ssl.get(c, span_rows, 1, s)) return rc;
     a.test_giveup = take_test_giveup(); // (the plain rows pass does not steal)
   }
   StealLease rsl; // RPCCRC_RAGGED_STEAL=1: the plain rows pass deals its tail from a steal counter too
@@ -702,7 +721,13 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     RPCCRC_TRY(launch_rows(a, 1, nt, mb, s, rsl.done_event(), &rsl.recorded));
     a.steal = nullptr;
   }
-  if (route) RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s, sl.p, sl.done_event(), &sl.recorded));
+  if (route) {
+    StealArgs span;
+    span.p = ssl.p;
+    span.done = ssl.done_event();
+    span.recorded = &ssl.recorded;
+    RPCCRC_TRY(launch_big_route(a, r, c.shift_nib, nt, mb, s, sl.p, sl.done_event(), &sl.recorded, span));
+  }
   return RPCCRC_OK;
 }
 
@@ -1354,7 +1379,7 @@ int rpc_frames_verify_device(const uint8_t *d_stream, uint64_t stream_bytes, con
   uint8_t *pre = ws + align256(n * 8) + 3 * align256(n * 4);
   RPCCRC_TRY(launch_frames_parse(d_stream, stream_bytes, d_frame_offsets, n, flags, boff, blen, bexp, pre, s));
   const bool lift = (flags & RPC_FRAMES_LIFT_CAP) != 0;
-  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift))) return rc;
+  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes))) return rc;
   return map_hip(launch_frames_compare(bcrc, bexp, pre, n, d_verdict, s));
 }
 
@@ -1378,7 +1403,7 @@ int rpc_frames_stamp_device(uint8_t *d_stream, uint64_t stream_bytes, const uint
   uint8_t *pre = d_verdict ? d_verdict : ws + align256(n * 8) + 2 * align256(n * 4);
   RPCCRC_TRY(launch_frames_stamp_prep(stream_bytes, d_frame_offsets, d_body_lens, n, flags, boff, blen, pre, s));
   const bool lift = (flags & RPC_FRAMES_LIFT_CAP) != 0;
-  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift))) return rc;
+  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes))) return rc;
   return map_hip(launch_frames_stamp(d_stream, d_frame_offsets, d_body_lens, bcrc, pre, n, version, type, s));
 }
 

@@ -270,6 +270,56 @@ def test_frames_lifted_cap_route_modes(n):
     assert got == expected(blob, offs, lift_cap=True)
 
 
+def aligned_stream(nbytes: int, align: int = 4096):
+    """A device byte buffer of nbytes whose first byte is `align`-aligned."""
+    t = torch.empty(nbytes + align, dtype=torch.uint8, device=DEV)
+    off = (-t.data_ptr()) % align
+    return t[off:off + nbytes]
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_frames_lifted_cap_span_mode(sparse):
+    """Route-all over a 4 KiB-aligned stream of >= 1 MiB: span mode (the bodies'
+    whole interior blocks from one uniform pass over the stream, their first and
+    last partial blocks from the fold, DESIGN.md 4.6) when the bodies are dense;
+    with 1 MiB gaps between frames the plan falls back to the chunk route.  Bodies
+    inside one block, across one boundary, ending on one, starting on one, spanning
+    many; every CRC and verdict against the oracle, stamp then verify, a flipped
+    byte in an interior block, the head and the tail of a long body."""
+    rng = np.random.default_rng(29 + sparse)
+    lens = [0, 1, 5, 4083, 4084, 4085, 4096 - HDR, 8192, 8193, 12288 - 7, 3 << 20, (2 << 20) + 4097, 77, 65536 + 3,
+            1 << 20, 4096, 4095, 16 << 20, 2, 40000]
+    lens += rng.integers(0, 20000, 40).tolist()
+    gap = (1 << 20) + 3 if sparse else 0
+    sizes = [HDR + L + gap for L in lens]
+    total = sum(sizes)
+    base = aligned_stream(total)
+    fill = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(fill, 0x5BA2)
+    base.copy_(fill[:total])
+    offs = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
+    do = to_dev(offs.view(np.int64))
+    dl = to_dev(np.array(lens, dtype=np.uint32).view(np.int32))
+    sv = rpc_amd.frames_stamp(base, do, dl, lift_cap=True, stream_bytes=total)
+    assert sv.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(lens)
+    host = base.cpu().numpy()
+    want = [oracle.crc32(host[int(o) + HDR:int(o) + HDR + L]) for o, L in zip(offs, lens)]
+    for o, L, c in zip(offs, lens, want):
+        assert host[int(o):int(o) + HDR].tobytes() == header(L, c)
+    v, c = rpc_amd.frames_verify(base, do, lift_cap=True, stream_bytes=total)
+    assert v.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(lens)
+    assert u32(c).tolist() == want
+    k = lens.index(16 << 20)
+    body0 = int(offs[k]) + HDR
+    flips = {k: [body0 + (5 << 20) + 123], 10: [int(offs[10]) + HDR + 1], 11: [int(offs[11]) + HDR + lens[11] - 1]}
+    for pos in sum(flips.values(), []):
+        base[pos] ^= 0x08
+    v, _ = rpc_amd.frames_verify(base, do, lift_cap=True, stream_bytes=total)
+    v = v.cpu().numpy().tolist()
+    assert [i for i, x in enumerate(v) if x != rpc_amd.FRAME_OK] == sorted(flips)
+    assert all(v[i] == rpc_amd.FRAME_BAD_CRC for i in flips)
+
+
 def test_frames_role_flags_rejected():
     d = to_dev(np.zeros(64, dtype=np.uint8))
     o = to_dev(np.zeros(1, dtype=np.int64))

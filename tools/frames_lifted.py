@@ -19,4 +19,5 @@ for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
     r["big_min"] = os.environ.get("RPCCRC_BIG_MIN", "default")
     r["big_aligned"] = os.environ.get("RPCCRC_BIG_ALIGNED", "default")
     r["big_chunk"] = os.environ.get("RPCCRC_BIG_CHUNK", "default")
+    r["big_span"] = os.environ.get("RPCCRC_BIG_SPAN", "default")
     print(json.dumps(r), flush=True)

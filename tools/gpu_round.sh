@@ -62,10 +62,10 @@ for s in $STEPS; do
            for k in ${FRAMES_CHUNKS:-4080 8176 16368}; do
              RPCCRC_BIG_CHUNK=$k run frames_chunk$k 300 python tools/frames_lifted.py 3 || exit 1
            done ;;
-    frames_ab) # interleaved: end-aligned (0) vs address-aligned (1) route chunks, and 16 KiB aligned chunks
+    frames_ab) # interleaved: route-all span mode on (1) / off (0, aligned 8 KiB chunks)
            for i in 1 2; do
-             for v in "0 8176" "1 8192" "1 16384"; do set -- $v
-               RPCCRC_BIG_ALIGNED=$1 RPCCRC_BIG_CHUNK=$2 run frames_a$1_c$2_$i 300 python tools/frames_lifted.py 2 || exit 1
+             for v in 1 0; do
+               RPCCRC_BIG_SPAN=$v run frames_span${v}_$i 300 python tools/frames_lifted.py 2 || exit 1
              done
            done ;;
     frames_libs) # lifted-cap frames probe per library (A/B): FRAMES_LIBS="head name ..."
