@@ -152,11 +152,26 @@ constexpr uint32_t kSvcPer = 2;                        // slots per wave: wave w
 constexpr uint32_t kSvcSlots = kSvcWaves * kSvcPer;    // concurrent drop-in calls served
 constexpr uint32_t kSvcMaxLen = 1024;                  // MAX_BODY_LEN (rpc.h:17)
 constexpr uint32_t kSvcStop = 0, kSvcExited = 1;       // SvcShared::ctl words
+constexpr uint32_t kSvcInline = 116;                   // bodies up to this length travel in the request block
+// A slot's request block: two 64-B lines the service reads in ONE poll.
+//   line 0: req = {len (low), seq (high)}, then inline bytes 0..55
+//   line 1: inline bytes 56..115, then tag
+// An inline body (len <= kSvcInline) ends at inline byte 116, so its CRC needs no
+// second PCIe round trip; longer bodies go to SvcShared::body.  Each line is read
+// whole (one cache line), but the two lines of one poll in no set order: the
+// host writes the bytes, then line 1's tag (= the request's seq), then line 0's
+// req word, and the service takes an inline request only when the tag matches
+// its seq (a line read whole shows a prefix of the host's stores to it).
+struct SvcReq {
+  uint64_t req;
+  uint8_t inl[kSvcInline];
+  uint32_t tag;
+};
+static_assert(sizeof(SvcReq) == 128, "two lines per request block");
 struct SvcShared {
-  // host: {len (low), seq (high)} of each slot, one store after the body; one
-  // 64-B line per slot (a shared line was written by up to 8 caller threads
+  // one block per slot (a shared line was written by up to 8 caller threads
   // while 8 waves polled it: 10 callers took 30 us a call, r04c)
-  uint64_t req[kSvcSlots][8];
+  SvcReq rq[kSvcSlots];
   uint64_t res[kSvcSlots][8];         // device: {crc, seq} (crc in the low half), one 64-B line per slot
   uint32_t ctl[16];                   // [kSvcStop] host: leave now; [kSvcExited] device: last instance that left
   uint8_t body[kSvcSlots][kSvcMaxLen]; // host: the body, right-aligned in 64 * seg bytes (seg 4 / 8 / 16)

@@ -876,18 +876,24 @@ __global__ void __launch_bounds__(256) big_expand_aligned_kernel(const uint8_t *
 // A_4(dword of window bytes [4t, 4t + 4)), the bytes before ps masked; the
 // window's crc0 is XOR_t A_{4 (1023 - t)}(term_t) (span_fold_terms + the
 // workgroup step).  The dword comes from two aligned loads through a buffer
-// resource starting at ps & ~3 (offsets before it wrap and read 0; none lies
-// past the dword holding byte pe - 1) and v_alignbyte.
+// resource starting at ps & ~3 (none lies past the dword holding byte pe - 1)
+// and v_alignbyte.  A dword before the resource gets kOobOffset, which fails
+// the range check and reads 0 -- NOT its wrapped offset: with constant-adjacent
+// offsets the two loads were merged into one 8-byte load, and a partly out-of-
+// range 8-byte load read 0 for the in-range dword too (r04e: every piece whose
+// first kept byte sat in the dword at ps & ~3 came out wrong).
 __device__ __forceinline__ uint32_t span_piece_term(const uint8_t *base, uint64_t ps, uint64_t pe, uint32_t t,
                                                     const uint32_t *a4) {
   const uint64_t B = ps & ~3ull;
   const uint32_t span = (uint32_t)(pe - B); // <= 4099
+  const uint32_t lim = (span + 3u) & ~3u;
   const uint32_t r = (uint32_t)pe & 3u;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base + B), (short)0,
-                                                                      (int)((span + 3u) & ~3u), 0x00020000);
-  const uint32_t a = span - 4096u + 4u * t - r; // aligned: window byte 4t lies at a + r
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)a, 0, 0);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a + 4u), 0, 0);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base + B), (short)0, (int)lim, 0x00020000);
+  const uint32_t a = span - 4096u + 4u * t - r; // aligned: window byte 4t lies at a + r (wraps before B)
+  const uint32_t lo_off = a < lim ? a : rows::kOobOffset, hi_off = a + 4u < lim ? a + 4u : rows::kOobOffset;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)lo_off, 0, 0);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)hi_off, 0, 0);
   const uint32_t wd = __builtin_amdgcn_alignbyte(hi, lo, r);
   const int d = (int)(4096u - (uint32_t)(pe - ps)) - (int)(4u * t); // bytes of this dword before ps
   const uint32_t keep = d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d)));

@@ -11,14 +11,17 @@
 //
 // Protocol (SvcShared, hipHostMallocCoherent: every access below bypasses the
 // GPU caches -- sc0 sc1 loads / stores, no cache-wide fence):
-//   host   writes the body right-aligned into body[slot] (virtual buffer of
-//          64 * seg bytes, seg = 4 / 8 / 16 bytes per lane by length), then
-//          req[slot] = {len, seq} as ONE 64-bit store (x86 stores stay in order);
-//   wave   polls the request words of its kSvcPer slots (one load, lane i =
-//          slot i); a seq it has not answered is a request: it reads the body
-//          (every lane its seg bytes; the loads of all its pending slots in
-//          flight together), computes the CRC and stores {crc, seq} into
-//          res[slot] (one 64-bit store);
+//   host   writes a body of <= kSvcInline bytes into the slot's request block
+//          (SvcReq: the tag, then the bytes, ending at inline byte 116), a
+//          longer one right-aligned into body[slot] (virtual buffer of 64 * seg
+//          bytes, seg = 4 / 8 / 16 bytes per lane by length), then
+//          rq[slot].req = {len, seq} as ONE 64-bit store (x86 stores stay in order);
+//   wave   polls the request blocks of its kSvcPer slots (one dword per lane,
+//          both blocks in one round trip); a seq it has not answered is a
+//          request (inline: once the block's tag equals it).  An inline body is
+//          already in registers; a longer one is read (every lane its seg bytes;
+//          the loads of all its pending slots in flight together).  It computes
+//          the CRC and stores {crc, seq} into res[slot] (one 64-bit store);
 //   host   spins on res[slot] until the seq matches.
 // The waves share the time of the last request in LDS (4 bytes) and all leave
 // after idle_ticks without one, after the kernel's lifetime cap, or when the
@@ -98,7 +101,7 @@ __device__ __forceinline__ uint32_t body_crc0(const Body &b, uint32_t seg, uint3
   return s;
 }
 
-__global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void crc32_service_kernel(
+__global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(48))) void crc32_service_kernel(
     SvcShared *sh, const uint32_t *tq, const uint32_t *kshift, uint64_t idle_ticks, uint64_t life_ticks,
     uint32_t instance) {
   __shared__ uint32_t s_last;  // low 32 bits of the last request's s_memrealtime
@@ -111,43 +114,65 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     s_alive = kSvcWaves;
   }
   __syncthreads();
+  static_assert(kSvcPer == 2, "one poll: 2 request blocks x 32 dwords");
   // per-lane constants: shift of this lane's segment to V's end, per seg class
   const uint32_t k4 = kshift[0 * 64 + lane], k8 = kshift[1 * 64 + lane], k16 = kshift[2 * 64 + lane];
   // wave w owns slots w + kSvcWaves * i (i < kSvcPer): the host hands slots out
-  // in index order, so concurrent callers land on different waves
-  const uint32_t myslot = wave + kSvcWaves * (lane < kSvcPer ? lane : 0u);
-  // lane i < kSvcPer: the seq this wave last answered for its slot i
-  uint32_t served = 0;
-  if (lane < kSvcPer)
-    served = (uint32_t)(__hip_atomic_load(&sh->res[myslot][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+  // lowest first, so concurrent callers land on different waves.  Poll: lane
+  // 32 i + d reads dword d of slot i's request block.
+  const uint32_t pslot = wave + kSvcWaves * (lane >> 5);
+  const uint32_t *pblk = reinterpret_cast<const uint32_t *>(&sh->rq[pslot]) + (lane & 31u);
+  // the seq this wave last answered for its slot i (wave-uniform)
+  uint32_t served[kSvcPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kSvcPer; ++i)
+    served[i] = (uint32_t)(__hip_atomic_load(&sh->res[wave + kSvcWaves * i][0], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+  // An inline body ends at block byte 124: V byte v (V = 256 B, seg 4) is block
+  // byte v - 132, so lane L's word is block dword L - 33 (lanes >= 33).
+  const int src0 = (int)lane - 33;
   for (uint32_t poll = 0;; ++poll) {
-    // one 64-bit word per slot, {len, seq}: the host stores it whole, after the body
-    const uint64_t rq =
-        (lane < kSvcPer) ? __hip_atomic_load(&sh->req[myslot][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
-    const uint32_t seq = (uint32_t)(rq >> 32);
-    uint64_t pend = __builtin_amdgcn_ballot_w64(lane < kSvcPer && seq != served);
-    if (pend != 0) {
-      // every pending slot's body loads first, then the CRCs
+    const uint32_t pv = ld_sys32(pblk); // both blocks, one round trip
+    uint32_t lens[kSvcPer], seqs[kSvcPer];
+    bool pend[kSvcPer], inl[kSvcPer];
+    bool any = false;
+#pragma unroll
+    for (uint32_t i = 0; i < kSvcPer; ++i) {
+      lens[i] = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 0));
+      seqs[i] = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 1));
+      const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 31));
+      if (lens[i] > kSvcMaxLen) lens[i] = kSvcMaxLen; // (the host never sends more)
+      inl[i] = lens[i] <= kSvcInline;
+      // an inline request counts once its block's second line (tag) is current
+      pend[i] = seqs[i] != served[i] && (!inl[i] || tag == seqs[i]);
+      any = any || pend[i];
+    }
+    if (any) {
+      // the longer bodies' loads first (a second round trip), then the CRCs
       Body body[kSvcPer];
-      uint32_t lens[kSvcPer], seqs[kSvcPer];
 #pragma unroll
       for (uint32_t i = 0; i < kSvcPer; ++i) {
-        const bool p = (pend >> i) & 1u;
-        lens[i] = p ? (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rq, (int)i) : 0u;
-        if (lens[i] > kSvcMaxLen) lens[i] = kSvcMaxLen; // (the host never sends more)
-        seqs[i] = (uint32_t)__builtin_amdgcn_readlane((int)seq, (int)i);
-        if (p) body[i] = load_body(sh->body[wave + kSvcWaves * i], svc::seg_of(lens[i]), lane);
+        if (pend[i] && !inl[i]) {
+          body[i] = load_body(sh->body[wave + kSvcWaves * i], svc::seg_of(lens[i]), lane);
+        } else {
+          // (every lane runs the shuffle: a lane outside the exec mask is not a
+          // source -- a shuffle under `src0 >= 0` read zeros from lanes 0..30)
+          const int src = src0 >= 0 ? (int)(32 * i) + src0 : (int)lane;
+          const uint32_t wv = (uint32_t)__shfl((int)pv, src, 64);
+          body[i].w[0] = src0 >= 0 ? wv : 0u; // (lanes < 33: before V's body, masked anyway)
+          body[i].w[1] = body[i].w[2] = body[i].w[3] = 0u;
+        }
       }
 #pragma unroll
       for (uint32_t i = 0; i < kSvcPer; ++i) {
-        if (!((pend >> i) & 1u)) continue;
+        if (!pend[i]) continue;
         const uint32_t len = lens[i], seg = svc::seg_of(len);
         const uint32_t c0 = body_crc0(body[i], seg, len, lane, seg == 4u ? k4 : seg == 8u ? k8 : k16);
         const uint32_t crc = len == 0u ? 0u : ~(tq[len] ^ c0);
         if (lane == 0)
           __hip_atomic_store(&sh->res[wave + kSvcWaves * i][0], (uint64_t)crc | ((uint64_t)seqs[i] << 32),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        served = (lane == i) ? seqs[i] : served;
+        served[i] = seqs[i];
       }
       if (lane == 0)
         __hip_atomic_store(&s_last, (uint32_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,

@@ -307,9 +307,11 @@ struct Service {
   const uint32_t *tq = nullptr;
   hipStream_t stream = nullptr;
   std::mutex launch_mu;
-  uint32_t launched = 0;       // instances launched (under launch_mu); instance k stores k when it leaves
-  std::mutex slot_mu;
-  std::vector<int> free_slots; // under slot_mu
+  std::atomic<uint32_t> launched{0}; // instances launched (written under launch_mu); instance k stores k when it leaves
+  // Slot k is held while bit k is set: a lock-free claim (a std::mutex free
+  // list put 10 concurrent callers to sleep on each other, r04d: 28 us a call).
+  // A thread first tries the slot it held last (the same wave, k % kSvcWaves).
+  std::atomic<uint32_t> busy{0};
   uint32_t seq[kSvcSlots] = {}; // last request seq of each slot (written by the slot's holder)
   bool ok = false;
 };
@@ -1025,7 +1027,6 @@ void svc_init(DeviceCtx &c) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking);
   (void)hipSetDevice(prev);
   v->tq = c.tq;
-  for (int i = kSvcSlots - 1; i >= 0; --i) v->free_slots.push_back(i); // slot 0 first: 8 callers on 8 waves
   v->ok = e == hipSuccess;
   if (v->ok) {
     std::lock_guard<std::mutex> g(g_services_mu);
@@ -1036,7 +1037,8 @@ void svc_init(DeviceCtx &c) {
 }
 
 bool svc_running(const Service &v) {
-  return *reinterpret_cast<const volatile uint32_t *>(&v.sh->ctl[kSvcExited]) != v.launched;
+  return *reinterpret_cast<const volatile uint32_t *>(&v.sh->ctl[kSvcExited]) !=
+         v.launched.load(std::memory_order_acquire);
 }
 
 // Launches an instance unless one is running (the new one queues behind a
@@ -1048,10 +1050,11 @@ bool svc_ensure(DeviceCtx &c, Service &v) {
   int prev = 0;
   (void)hipGetDevice(&prev);
   if (prev != c.device) (void)hipSetDevice(c.device);
-  const hipError_t e = launch_service(v.sh, v.tq, v.kshift, kSvcIdleTicks, kSvcLifeTicks, v.launched + 1, v.stream);
+  const uint32_t next = v.launched.load(std::memory_order_relaxed) + 1;
+  const hipError_t e = launch_service(v.sh, v.tq, v.kshift, kSvcIdleTicks, kSvcLifeTicks, next, v.stream);
   if (prev != c.device) (void)hipSetDevice(prev);
   if (e != hipSuccess) return false;
-  ++v.launched;
+  v.launched.store(next, std::memory_order_release);
   return true;
 }
 
@@ -1062,20 +1065,33 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
   std::call_once(c.svc_once, svc_init, std::ref(c));
   Service &v = *c.svc;
   if (!v.ok) return false;
+  // claim a slot: this thread's last one if free, else the lowest free one
+  thread_local int last_slot = -1;
   int slot = -1;
-  {
-    std::lock_guard<std::mutex> g(v.slot_mu);
-    if (v.free_slots.empty()) return false;
-    slot = v.free_slots.back();
-    v.free_slots.pop_back();
+  for (uint32_t m = v.busy.load(std::memory_order_relaxed);;) {
+    const uint32_t free = ~m & ((1u << kSvcSlots) - 1u);
+    if (free == 0) return false;
+    const int k = (last_slot >= 0 && ((free >> last_slot) & 1u)) ? last_slot : __builtin_ctz(free);
+    if (v.busy.compare_exchange_weak(m, m | (1u << k), std::memory_order_acquire, std::memory_order_relaxed)) {
+      slot = k;
+      break;
+    }
   }
+  last_slot = slot;
   SvcShared *sh = v.sh;
-  const uint32_t seg = svc::seg_of(len);
-  memcpy(sh->body[slot] + 64u * seg - len, src, len);
+  SvcReq &rq = sh->rq[slot];
   uint32_t q = ++v.seq[slot];
   if (q == 0) q = ++v.seq[slot]; // 0: the answered seq of a fresh slot
+  if (len <= kSvcInline) { // in the request block, ending at its inline byte 116; then line 1's tag
+    memcpy(rq.inl + kSvcInline - len, src, len);
+    std::atomic_thread_fence(std::memory_order_release);
+    *reinterpret_cast<volatile uint32_t *>(&rq.tag) = q;
+  } else {
+    const uint32_t seg = svc::seg_of(len);
+    memcpy(sh->body[slot] + 64u * seg - len, src, len);
+  }
   std::atomic_thread_fence(std::memory_order_release); // the body before the request word (x86: a compiler barrier)
-  *reinterpret_cast<volatile uint64_t *>(&sh->req[slot][0]) = (uint64_t)len | ((uint64_t)q << 32);
+  *reinterpret_cast<volatile uint64_t *>(&rq.req) = (uint64_t)len | ((uint64_t)q << 32);
   bool ok = svc_ensure(c, v);
   const volatile uint64_t *res = &sh->res[slot][0];
   uint64_t r = *res;
@@ -1094,10 +1110,7 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
       }
     }
   }
-  {
-    std::lock_guard<std::mutex> g(v.slot_mu);
-    v.free_slots.push_back(slot);
-  }
+  v.busy.fetch_and(~(1u << slot), std::memory_order_release);
   if (ok) *crc = (uint32_t)r;
   return ok;
 }

@@ -215,6 +215,33 @@ def test_drop_in_thread_safety():
     assert not errors
 
 
+def test_drop_in_service_stress_inline_boundary():
+    """The drop-in service's request blocks (crc32_kernels.h SvcReq): bodies of up
+    to 116 B travel inline in two request lines validated by a tag, longer ones in
+    the body area.  10 threads x 3000 back-to-back calls on their slots, lengths
+    0..240 around the inline bound, each body differing from the slot's previous
+    one, every CRC against the oracle (a torn or stale line would show)."""
+    rng = np.random.default_rng(17)
+    pool = rng.integers(0, 256, 1 << 16, dtype=np.uint8).tobytes()
+    errors = []
+
+    def worker(k):
+        r = np.random.default_rng(100 + k)
+        for _ in range(3000):
+            L = int(r.integers(0, 241))
+            o = int(r.integers(0, len(pool) - L))
+            b = pool[o:o + L]
+            if rpc_amd.rpc_crc32(b) != oracle.crc32(np.frombuffer(b, dtype=np.uint8)):
+                errors.append((k, L))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(10)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:10]
+
+
 # ---- device batches ------------------------------------------------------------
 
 @pytest.mark.parametrize("body_len", [1, 3, 4, 15, 16, 17, 63, 64, 100, 1000, 1023, 1024, 1025, 2000, 4080,
@@ -851,17 +878,22 @@ def test_drop_in_service_beside_batches():
     wants = [oracle.crc32(b) for b in bodies]
 
     def timed(reps=20):
+        # per-launch event pairs, enqueued behind ~1 ms of other batches so that
+        # a caller thread slowed by the hammering thread (the GIL) does not open
+        # gaps: the median launch is the kernel's own time
         s = torch.cuda.current_stream()
-        rpc_amd.device_uniform(x, n, L)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
+        for _ in range(6):
+            rpc_amd.device_uniform(x, n, L)
+        ev = []
         for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
             out = rpc_amd.device_uniform(x, n, L)
-        e1.record(s)
-        e1.synchronize()
+            e1.record(s)
+            ev.append((e0, e1))
+        ev[-1][1].synchronize()
         assert np.array_equal(u32(out), want)
-        return e0.elapsed_time(e1) / reps
+        return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
     alone = min(timed() for _ in range(3))
     errors, calls = [], [0]
