@@ -101,10 +101,17 @@ struct BigRoute {
   // when the plan finds the bodies dense in [base, base + 4096 * span_rows_max)
   // (meta[5] = 1), the UNIFORM rows pass CRCs every whole 4 KiB block below the
   // last body end into blk[] (meta[4] blocks), the ragged chunk pass has no
-  // chunks, and the fold takes a body's interior blocks from blk[] and its
-  // first / last partial block from the bytes themselves.
+  // chunks, and the fold takes a body's interior blocks from blk[] and CRCs its
+  // first / last partial blocks itself.
   uint32_t *blk = nullptr;
   uint64_t span_rows_max = 0;
+  const uint4 *tab4 = nullptr; // span mode: the slice-by-4 tables (scalar table image, first 4 KiB)
+  // Frames verify in route-all mode: the fold also decides each frame's verdict
+  // (frames_compare_kernel's rule: the parse's pre-verdict, else crc == the
+  // header's crc32), so the compare launch is skipped.  nullptr: no verdicts.
+  const uint32_t *cmp_expected = nullptr;
+  const uint8_t *cmp_pre = nullptr;
+  uint8_t *cmp_verdict = nullptr;
   const uint32_t *dbl = nullptr; // kBigDblWords: the fold's doubling maps per chunk class (build_big_dbl)
 };
 // (The fold's doubling maps per chunk class: crc32_layout.h build_big_dbl.)

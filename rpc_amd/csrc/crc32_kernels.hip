@@ -27,6 +27,8 @@
 #include "crc32_layout.h"
 #include "crc32_packed.h"
 #include "crc32_rows.h"
+#include "frames.h"
+#include "../../include/rpccrc.h"
 
 namespace rpccrc {
 
@@ -850,7 +852,8 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
 
 __global__ void __launch_bounds__(256) big_expand_aligned_kernel(const uint8_t *base, const uint64_t *offsets,
                                                                  const uint32_t *lengths, BigRoute r) {
-  const uint64_t nb = (r.span_rows_max != 0 && r.meta[5] != 0) ? 0 : big_count(r), chunk = r.meta[3];
+  if (r.span_rows_max != 0 && r.meta[5] != 0) return; // span mode: no chunk table
+  const uint64_t nb = big_count(r), chunk = r.meta[3];
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint32_t i = big_body(r, b);
@@ -868,60 +871,84 @@ __global__ void __launch_bounds__(256) big_expand_aligned_kernel(const uint8_t *
 // ---- span mode (BigRoute.span_rows_max; route-all batches) --------------------
 // A body [s, e) (offsets from the 4 KiB-aligned base) covers blocks j0..j1: its
 // chunks are the aligned chunks of C = 4096 -- the first and last partial
-// blocks, whose crc0 the fold computes here from the bytes, and the interior
-// blocks j0 < j < j1, whose crc0 the span pass (uniform rows, RAW) left in blk[j].
+// blocks, which the fold CRCs itself (span_piece_wave, one wave each), and the
+// interior blocks j0 < j < j1, whose crc0 the span pass (uniform rows, RAW)
+// left in blk[j].  (Round 4 tried the two pieces as a window over all 1024
+// threads with two block-wide reductions -- fold 43.6 us for 1024 frames -- and
+// as items of the ragged chunk pass -- 16.4 us for that pass:
+// profiles/r04e, r04f prof_frames.)
 //
-// crc0 of a piece [ps, pe) of <= 4096 bytes, right-aligned in a 4096-byte
-// window (leading zeros leave crc0 unchanged): thread t's term is
-// A_4(dword of window bytes [4t, 4t + 4)), the bytes before ps masked; the
-// window's crc0 is XOR_t A_{4 (1023 - t)}(term_t) (span_fold_terms + the
-// workgroup step).  The dword comes from two aligned loads through a buffer
-// resource starting at ps & ~3 (none lies past the dword holding byte pe - 1)
-// and v_alignbyte.  A dword before the resource gets kOobOffset, which fails
-// the range check and reads 0 -- NOT its wrapped offset: with constant-adjacent
-// offsets the two loads were merged into one 8-byte load, and a partly out-of-
-// range 8-byte load read 0 for the in-range dword too (r04e: every piece whose
-// first kept byte sat in the dword at ps & ~3 came out wrong).
-__device__ __forceinline__ uint32_t span_piece_term(const uint8_t *base, uint64_t ps, uint64_t pe, uint32_t t,
-                                                    const uint32_t *a4) {
+// crc0 of a piece [ps, pe) of <= 4096 bytes by ONE wave: the piece right-
+// aligned in a 4096-byte window (leading zeros leave crc0 unchanged), lane L
+// takes window bytes [64 L, 64 L + 64): 16 slice-by-4 steps from T (the
+// scalar kernel's tables, T_k at T + 256 k), then six pair levels, the left
+// group shifted past the right one's 64 * 2^b bytes by NIB[6 + b].  The words
+// come from 17 aligned dword loads per lane through a buffer resource based at
+// ps & ~3 and v_alignbyte; a dword before the resource gets kOobOffset (reads
+// 0 without an access) -- not its wrapped offset, which with constant-adjacent
+// offsets merged two loads into one partly out-of-range load that read 0 for
+// the in-range dword too (r04e); bytes before ps are masked.
+constexpr uint32_t kFoldThreads = 256, kFoldLog2 = 8, kFoldWaves = kFoldThreads / 64;
+// Raw chunk CRCs each thread loads before its Horner steps (a 64 MiB body in
+// 4 KiB span blocks is 64 steps per thread: 2 round trips, 8 with 8 in flight).
+constexpr uint32_t kFoldBatch = 32;
+// BigRoute.cmp_*: frames_compare_kernel's rule, in the fold (route-all frames verify).
+__device__ __forceinline__ void fold_verdict(const BigRoute &r, uint32_t i, uint32_t crc) {
+  const uint8_t p = r.cmp_pre[i];
+  r.cmp_verdict[i] = (p != kFramePending) ? p : (crc == r.cmp_expected[i] ? RPC_FRAME_OK : RPC_FRAME_BAD_CRC);
+}
+static_assert((1u << kFoldLog2) == kFoldThreads && kFoldThreads == 256, "T4 load: one uint4 per thread");
+
+__device__ __forceinline__ uint32_t span_piece_wave(const uint8_t *base, uint64_t ps, uint64_t pe, uint32_t lane,
+                                                    const uint32_t *T, const uint32_t *nib) {
   const uint64_t B = ps & ~3ull;
   const uint32_t span = (uint32_t)(pe - B); // <= 4099
   const uint32_t lim = (span + 3u) & ~3u;
   const uint32_t r = (uint32_t)pe & 3u;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base + B), (short)0, (int)lim, 0x00020000);
-  const uint32_t a = span - 4096u + 4u * t - r; // aligned: window byte 4t lies at a + r (wraps before B)
-  const uint32_t lo_off = a < lim ? a : rows::kOobOffset, hi_off = a + 4u < lim ? a + 4u : rows::kOobOffset;
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)lo_off, 0, 0);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)hi_off, 0, 0);
-  const uint32_t wd = __builtin_amdgcn_alignbyte(hi, lo, r);
-  const int d = (int)(4096u - (uint32_t)(pe - ps)) - (int)(4u * t); // bytes of this dword before ps
-  const uint32_t keep = d <= 0 ? 0xFFFFFFFFu : (d >= 4 ? 0u : (0xFFFFFFFFu << (8 * d)));
-  return nib_map(a4, wd & keep);
-}
-// In-wave step: lanes hold crc0 of consecutive dwords; after the level of
-// distance d a lane holds its 2d-dword group's crc0 (the left half shifted
-// past the right half's 4d bytes by NIB[log2 4d]).
-__device__ __forceinline__ uint32_t span_fold_terms(uint32_t v, uint32_t lane, const uint32_t *nib) {
+  const uint32_t a0 = span - 4096u + 64u * lane - r; // aligned; wraps before B
+  const int kmin = (int)(4096u - (uint32_t)(pe - ps)); // window bytes before the piece
+  uint32_t d[17];
 #pragma unroll
-  for (uint32_t d = 1, k = 2; d < 64; d <<= 1, ++k) {
-    const uint32_t sh = nib_map(nib + 128u * k, v);
-    const uint32_t mine = (lane & d) ? v : sh;
-    v = mine ^ (uint32_t)__shfl_xor((int)mine, (int)d, 64);
+  for (uint32_t k = 0; k < 17; ++k) {
+    const uint32_t off = a0 + 4u * k;
+    d[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off < lim ? off : rows::kOobOffset), 0, 0);
   }
-  return v;
+  uint32_t sv = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint32_t wd = __builtin_amdgcn_alignbyte(d[k + 1], d[k], r);
+    const int dd = kmin - (int)(64u * lane + 4u * k); // bytes of this word before ps
+    const uint32_t keep = dd <= 0 ? 0xFFFFFFFFu : (dd >= 4 ? 0u : (0xFFFFFFFFu << (8 * dd)));
+    const uint32_t x = sv ^ (wd & keep);
+    sv = T[768 + (x & 0xFFu)] ^ T[512 + ((x >> 8) & 0xFFu)] ^ T[256 + ((x >> 16) & 0xFFu)] ^ T[x >> 24];
+  }
+#pragma unroll
+  for (uint32_t b = 0; b < 6; ++b) {
+    const uint32_t sh = nib_map(nib + 128u * (6u + b), sv);
+    const uint32_t mine = ((lane >> b) & 1u) ? sv : sh;
+    sv = mine ^ (uint32_t)__shfl_xor((int)mine, 1 << b, 64);
+  }
+  return sv;
 }
 
 // Block b folds routed bodies b, b + grid, ...: thread t runs Horner over
-// chunks t, t + 1024, ... of the first nch - 1 with the step map A_{1024 C},
-// shifts its partial by A_{j C} (j < 1024 chunks after its last one), and the
-// block XOR-reduces into G; thread 0 adds the last chunk.  All maps are the
-// power-of-two shifts NIB[k] = A_{2^k bytes} (32 KiB, in LDS).
-__global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t *base, const uint64_t *offsets,
+// chunks t, t + T, ... of the first nch - 1 with the step map A_{T C} (T =
+// kFoldThreads), shifts its partial by A_{j C} (j < T chunks after its last
+// one), and the block XOR-reduces into G; thread 0 adds the last chunk.  All
+// maps are the power-of-two shifts NIB[k] = A_{2^k bytes} (32 KiB, in LDS).
+// T = 256 (round 4; 1024 before): a block's cost is mostly fixed -- the map
+// table, the two partial blocks (span mode), thread 0's final shifts -- and a
+// frames batch has one body per block, so 4x more resident blocks beat 4x
+// longer Horner chains on the few long bodies (1024 frames: fold 35.9 us at
+// 1024 threads, profiles/r04h prof_frames).
+__global__ void __launch_bounds__(kFoldThreads) big_combine_aligned_kernel(const uint8_t *base, const uint64_t *offsets,
                                                                    const uint32_t *lengths, BigRoute r,
                                                                    const uint4 *shift_nib, uint32_t *out) {
   __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
-  __shared__ uint32_t part[16], part2[16], praw[2];
+  __shared__ __attribute__((aligned(16))) uint32_t T4[1024]; // span mode: slice-by-4 tables (r.tab4)
+  __shared__ uint32_t part[kFoldWaves], praw[2];
   const uint64_t nb = big_count(r);
   if (blockIdx.x >= nb) return;
   const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
@@ -931,76 +958,65 @@ __global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t
   {
     uint4 *dst = reinterpret_cast<uint4 *>(nib);
 #pragma unroll
-    for (uint32_t q = 0; q < kShiftNibWords / 4 / 1024; ++q) dst[q * 1024 + t] = shift_nib[q * 1024 + t];
+    for (uint32_t q = 0; q < kShiftNibWords / 4 / kFoldThreads; ++q)
+      dst[q * kFoldThreads + t] = shift_nib[q * kFoldThreads + t];
+    if (span) reinterpret_cast<uint4 *>(T4)[t] = r.tab4[t];
   }
   __syncthreads();
   auto apply = [&](uint64_t nbytes, uint32_t v) { // A_nbytes(v): one map per set bit
     for (; nbytes; nbytes &= nbytes - 1) v = nib_map(nib + 128u * (uint32_t)__builtin_ctzll(nbytes), v);
     return v;
   };
-  const uint32_t *stepnib = nib + 128u * (lc + 10u); // A_{1024 C}
+  const uint32_t *stepnib = nib + 128u * (lc + kFoldLog2); // A_{kFoldThreads C}
   const uint64_t b0 = (uint64_t)(uintptr_t)base;
   for (uint64_t b = blockIdx.x; span && b < nb; b += gridDim.x) { // span mode (block-uniform)
     const uint32_t i = (uint32_t)b; // route-all: body b
     const uint64_t s = offsets[i], L = lengths[i], e = s + L;
     const uint64_t j0 = s >> 12, j1 = L ? (e - 1) >> 12 : j0, nch = L ? j1 - j0 + 1 : 0;
-    // the first and last partial blocks' crc0 (one piece: the body lies in one block)
-    uint32_t v0 = 0, v1 = 0;
-    if (L) {
-      v0 = span_piece_term(base, s, nch == 1 ? e : (j0 + 1) << 12, t, nib + 128u * 2u);
-      if (nch > 1) v1 = span_piece_term(base, j1 << 12, e, t, nib + 128u * 2u);
-    }
-    v0 = span_fold_terms(v0, lane, nib);
-    v1 = span_fold_terms(v1, lane, nib);
-    if (lane == 0) {
-      part[w] = v0;
-      part2[w] = v1;
-    }
-    __syncthreads();
-    if (t == 0) { // the 16 waves' 256-B groups, A_256 = NIB[8]
-      uint32_t h = 0, g = 0;
-      for (uint32_t k = 0; k < 16; ++k) {
-        h = nib_map(nib + 128u * 8u, h) ^ part[k];
-        g = nib_map(nib + 128u * 8u, g) ^ part2[k];
-      }
-      praw[0] = h;
-      praw[1] = g;
-    }
-    __syncthreads();
-    const uint32_t head = praw[0], tail = praw[1];
-    uint32_t seed = 0; // A_{len0}(F): zlib's pre-conditioning enters with the first piece
-    if (t == 0 && nch != 0) {
-      const uint64_t len0 = (nch == 1 ? e : (j0 + 1) << 12) - s;
-      seed = apply(len0 & ~4095ull, r.tq[len0 & 4095u]);
+    const uint64_t h_end = nch == 1 ? e : (j0 + 1) << 12;
+    // waves 0 / 1: the first / last partial block, while the others fold the
+    // interior blocks (G' below leaves chunk 0, the head, to thread 0 at the end)
+    if (w < 2u) {
+      uint32_t v = 0;
+      if (w == 0u && nch != 0) v = span_piece_wave(base, s, h_end, lane, T4, nib);
+      if (w == 1u && nch > 1) v = span_piece_wave(base, j1 << 12, e, lane, T4, nib);
+      if (lane == 0) praw[w] = v;
     }
     const uint64_t m = nch ? nch - 1 : 0; // chunks folded into G: the head, then blocks j0 + 1 ..
     uint32_t acc = 0;
-    constexpr uint32_t kB = 8;
-    for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * 1024u) {
+    constexpr uint32_t kB = kFoldBatch;
+    for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * kFoldThreads) {
       uint32_t rv[kB];
 #pragma unroll
       for (uint32_t q = 0; q < kB; ++q) {
-        const uint64_t k = k0 + q * 1024u;
-        rv[q] = k == 0 ? head : (k < m ? r.blk[j0 + k] : 0u);
+        const uint64_t k = k0 + q * kFoldThreads;
+        rv[q] = (k != 0 && k < m) ? r.blk[j0 + k] : 0u;
       }
 #pragma unroll
       for (uint32_t q = 0; q < kB; ++q)
-        if (k0 + q * 1024u < m) acc = nib_map(stepnib, acc) ^ rv[q] ^ (k0 + q == 0 ? seed : 0u);
+        if (k0 + q * kFoldThreads < m) acc = nib_map(stepnib, acc) ^ rv[q];
     }
     if (t < m) {
-      for (uint32_t j = (uint32_t)((m - 1 - t) % 1024u); j; j &= j - 1)
+      for (uint32_t j = (uint32_t)((m - 1 - t) % kFoldThreads); j; j &= j - 1)
         acc = nib_map(nib + 128u * (lc + (uint32_t)__builtin_ctz(j)), acc);
     }
     for (int d = 1; d < 64; d <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, d, 64);
-    __syncthreads(); // (part[] was read above)
     if (lane == 0) part[w] = acc;
     __syncthreads();
     if (t == 0) {
-      for (uint32_t k = 1; k < 16; ++k) acc ^= part[k];
+      for (uint32_t k = 1; k < kFoldWaves; ++k) acc ^= part[k];
+      // zlib's pre-conditioning enters with the head: A_{len0}(F)
+      const uint64_t len0 = h_end - s;
+      const uint32_t head = praw[0] ^ apply(len0 & ~4095ull, r.tq[len0 & 4095u]);
       uint32_t crc = 0;
-      if (nch == 1) crc = ~(head ^ seed);
-      else if (nch > 1) crc = ~(apply(e - (j1 << 12), acc) ^ tail);
+      if (nch == 1) {
+        crc = ~head;
+      } else if (nch > 1) {
+        const uint32_t g = acc ^ apply((m - 1) << 12, head); // + the head, m - 1 chunks before the last of G
+        crc = ~(apply(e - (j1 << 12), g) ^ praw[1]);
+      }
       out[i] = crc; // an empty body: crc32 = 0
+      if (r.cmp_verdict) fold_verdict(r, i, crc);
     }
     __syncthreads();
   }
@@ -1017,24 +1033,24 @@ __global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t
     }
     const uint64_t m = nch ? nch - 1 : 0; // chunks folded into G
     uint32_t acc = 0;
-    constexpr uint32_t kB = 8;
-    for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * 1024u) {
+    constexpr uint32_t kB = kFoldBatch;
+    for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * kFoldThreads) {
       uint32_t rv[kB];
 #pragma unroll
-      for (uint32_t q = 0; q < kB; ++q) rv[q] = (k0 + q * 1024u < m) ? r.c_raw[first + k0 + q * 1024u] : 0u;
+      for (uint32_t q = 0; q < kB; ++q) rv[q] = (k0 + q * kFoldThreads < m) ? r.c_raw[first + k0 + q * kFoldThreads] : 0u;
 #pragma unroll
       for (uint32_t q = 0; q < kB; ++q)
-        if (k0 + q * 1024u < m) acc = nib_map(stepnib, acc) ^ rv[q] ^ (k0 + q == 0 ? seed : 0u);
+        if (k0 + q * kFoldThreads < m) acc = nib_map(stepnib, acc) ^ rv[q] ^ (k0 + q == 0 ? seed : 0u);
     }
     if (t < m) { // chunks between this thread's last one and chunk m - 1
-      for (uint32_t j = (uint32_t)((m - 1 - t) % 1024u); j; j &= j - 1)
+      for (uint32_t j = (uint32_t)((m - 1 - t) % kFoldThreads); j; j &= j - 1)
         acc = nib_map(nib + 128u * (lc + (uint32_t)__builtin_ctz(j)), acc);
     }
     for (int d = 1; d < 64; d <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, d, 64);
     if ((t & 63u) == 0) part[t >> 6] = acc;
     __syncthreads();
     if (t == 0) {
-      for (uint32_t w = 1; w < 16; ++w) acc ^= part[w];
+      for (uint32_t w = 1; w < kFoldWaves; ++w) acc ^= part[w];
       uint32_t crc = 0;
       if (nch == 1) {
         crc = ~(r.c_raw[first] ^ seed);
@@ -1043,6 +1059,7 @@ __global__ void __launch_bounds__(1024) big_combine_aligned_kernel(const uint8_t
         crc = ~(apply(e - last_lo, acc) ^ r.c_raw[first + nch - 1]);
       }
       out[i] = crc; // an empty body: crc32 = 0
+      if (r.cmp_verdict) fold_verdict(r, i, crc);
     }
     __syncthreads();
   }
@@ -1094,7 +1111,7 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
   if (proto.n_items == 0) return hipSuccess;
   if (proto.mode != kModeFinal || proto.offsets == nullptr || proto.lengths == nullptr || !r.tq) return hipErrorInvalidValue;
   // span mode: route-all over a 4 KiB-aligned base, aligned chunks, a block table
-  if (r.span_rows_max != 0 && (!r.all_n || !r.aligned || !r.blk || ((uintptr_t)proto.base & 4095u) != 0 ||
+  if (r.span_rows_max != 0 && (!r.all_n || !r.aligned || !r.blk || !r.tab4 || ((uintptr_t)proto.base & 4095u) != 0 ||
                                r.span_rows_max > kSpanMaxRows))
     return hipErrorInvalidValue;
   hipError_t e;
@@ -1158,7 +1175,7 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
   // 1024 blocks (blocks past the routed-body count leave at once): a block folds
   // one body at a time, so the count bounds the serial bodies per block.
   if (r.aligned)
-    hipLaunchKernelGGL(big_combine_aligned_kernel, dim3(1024), dim3(1024), 0, s, proto.base, proto.offsets,
+    hipLaunchKernelGGL(big_combine_aligned_kernel, dim3(2048), dim3(kFoldThreads), 0, s, proto.base, proto.offsets,
                        proto.lengths, r, shift_nib, proto.out);
   else
     hipLaunchKernelGGL(big_combine_kernel, dim3(1024), dim3(1024), 0, s, proto.lengths, r, shift_nib, proto.out);

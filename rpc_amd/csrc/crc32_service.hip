@@ -30,7 +30,8 @@
 // that arrives while an instance is leaving is picked up by the next one:
 // pending = seq not yet answered in res).
 //
-// Resources: NO table image in LDS and few registers, so the kernel can sit
+// Resources: NO table image in LDS and few registers (37 VGPRs; built without
+// the library's max-ilp scheduler, Makefile), so the kernel can sit
 // on a CU next to a rows-kernel workgroup (155 KiB LDS each, one per CU, a
 // persistent grid over all CUs): the CRC is bit-serial --
 //   chain: crc0 of each 32-bit word by the bit loop (3 VALU per bit);
@@ -101,7 +102,7 @@ __device__ __forceinline__ uint32_t body_crc0(const Body &b, uint32_t seg, uint3
   return s;
 }
 
-__global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8), amdgpu_num_vgpr(48))) void crc32_service_kernel(
+__global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void crc32_service_kernel(
     SvcShared *sh, const uint32_t *tq, const uint32_t *kshift, uint64_t idle_ticks, uint64_t life_ticks,
     uint32_t instance) {
   __shared__ uint32_t s_last;  // low 32 bits of the last request's s_memrealtime
@@ -148,7 +149,8 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
       any = any || pend[i];
     }
     if (any) {
-      // the longer bodies' loads first (a second round trip), then the CRCs
+      // the longer bodies' loads first (a second round trip, both slots' in
+      // flight together), then the CRCs
       Body body[kSvcPer];
 #pragma unroll
       for (uint32_t i = 0; i < kSvcPer; ++i) {

@@ -629,9 +629,16 @@ int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, cons
 //    does not stream through a single wave.  Not with the packed kernel.
 //  * span_bytes (frames calls: the stream length; 0 otherwise): a route-all
 //    batch over a 4 KiB-aligned base may take the route's span mode (BigRoute).
+//  * cmp (frames verify): in route-all mode the fold writes the verdicts too
+//    and *compared is set (the caller then skips its compare launch).
+struct FramesCmp {
+  const uint32_t *expected;
+  const uint8_t *pre;
+  uint8_t *verdict;
+};
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
            uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route, uint32_t *err = nullptr,
-           uint64_t span_bytes = 0) {
+           uint64_t span_bytes = 0, const FramesCmp *cmp = nullptr, bool *compared = nullptr) {
   const int path = g_ragged_path.load(std::memory_order_relaxed);
   const bool nt = nontemporal();
   const int mb = max_blocks_for(c);
@@ -696,8 +703,15 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     r.aligned = g_big_aligned;
     r.tq = c.tq;
     r.dbl = c.big_dbl;
+    r.tab4 = c.scalar_tab;
     if (route_all) {
       r.all_n = (uint32_t)n;
+      if (cmp) {
+        r.cmp_expected = cmp->expected;
+        r.cmp_pre = cmp->pre;
+        r.cmp_verdict = cmp->verdict;
+        if (compared) *compared = true;
+      }
     } else {
       const uint32_t big_min = big_min_for(n);
       RPCCRC_TRY(launch_big_classify(lengths, n, big_min, r, s));
@@ -1392,7 +1406,11 @@ int rpc_frames_verify_device(const uint8_t *d_stream, uint64_t stream_bytes, con
   uint8_t *pre = ws + align256(n * 8) + 3 * align256(n * 4);
   RPCCRC_TRY(launch_frames_parse(d_stream, stream_bytes, d_frame_offsets, n, flags, boff, blen, bexp, pre, s));
   const bool lift = (flags & RPC_FRAMES_LIFT_CAP) != 0;
-  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes))) return rc;
+  const FramesCmp cmp{bexp, pre, d_verdict};
+  bool compared = false;
+  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes, &cmp, &compared)))
+    return rc;
+  if (compared) return RPCCRC_OK; // (route-all: the fold wrote the verdicts)
   return map_hip(launch_frames_compare(bcrc, bexp, pre, n, d_verdict, s));
 }
 

@@ -213,49 +213,8 @@ def test_aligned_fold_matches_zlib(L, start, chunk, nt):
 
 # ---- span mode (big_combine_aligned_kernel span branch) -----
 # The bodies lie in a 4 KiB-aligned stream; the span pass CRCs every whole 4 KiB
-# block (RAW) and the fold takes a body's interior blocks from it.  The first and
-# last partial blocks are CRC'd by the fold itself: a piece [ps, pe) right-aligned
-# in a 4096-byte window, thread t's term A_4(dword of window bytes 4t..4t+3) with
-# the bytes before ps masked, the dword assembled from two aligned loads through a
-# buffer resource based at ps & ~3 (range align4(pe - base), wrapped offsets read
-# 0) by v_alignbyte; then 6 in-wave levels (left half shifted by NIB[log2 4d]) and
-# a Horner over the 16 waves' 256-B groups with A_256.
-
-
-def span_piece_emulated(mem: bytes, ps: int, pe: int) -> int:
-    B = ps & ~3
-    span = pe - B
-    r = pe & 3
-    nrec = (span + 3) & ~3
-
-    def ld32(off):
-        off &= 0xFFFFFFFF
-        if off + 4 > nrec:
-            return 0
-        return int.from_bytes(mem[B + off:B + off + 4].ljust(4, b"\0"), "little")
-
-    terms = []
-    for t in range(1024):
-        a = (span - 4096 + 4 * t - r) & 0xFFFFFFFF
-        lo, hi = ld32(a), ld32(a + 4)
-        wd = ((hi << 32 | lo) >> (8 * r)) & 0xFFFFFFFF
-        d = (4096 - (pe - ps)) - 4 * t
-        keep = 0xFFFFFFFF if d <= 0 else (0 if d >= 4 else (0xFFFFFFFF << (8 * d)) & 0xFFFFFFFF)
-        terms.append(nib_apply(2, wd & keep))
-    parts = []
-    for w in range(16):
-        v = terms[64 * w:64 * w + 64]
-        d, k = 1, 2
-        while d < 64:
-            mine = [v[l] if l & d else nib_apply(k, v[l]) for l in range(64)]
-            v = [mine[l] ^ mine[l ^ d] for l in range(64)]
-            d, k = d * 2, k + 1
-        assert len(set(v)) == 1  # every lane holds the wave's crc0
-        parts.append(v[0])
-    h = 0
-    for p in parts:
-        h = nib_apply(8, h) ^ p
-    return h
+# block (RAW) and the fold takes a body's interior blocks from it.  The ragged
+# chunk pass CRCs each body's first and last partial blocks (pieces 2b, 2b + 1).
 
 
 def span_fold_emulated(mem: bytes, s: int, L: int, nt: int) -> int:
@@ -264,32 +223,25 @@ def span_fold_emulated(mem: bytes, s: int, L: int, nt: int) -> int:
     e = s + L
     j0, j1 = s >> 12, (e - 1) >> 12
     nch = j1 - j0 + 1
-    head = span_piece_emulated(mem, s, e if nch == 1 else (j0 + 1) << 12)
-    tail = span_piece_emulated(mem, j1 << 12, e) if nch > 1 else 0
+    head = crc0(mem[s:e if nch == 1 else (j0 + 1) << 12])
+    tail = crc0(mem[j1 << 12:e]) if nch > 1 else 0
     len0 = (e if nch == 1 else (j0 + 1) << 12) - s
     seed = nib_shift(len0 & ~4095, nib_shift(len0 & 4095, 0xFFFFFFFF))
     if nch == 1:
         return ~(head ^ seed) & 0xFFFFFFFF
     m = nch - 1
-    raw = [head] + [crc0(mem[(j0 + k) << 12:(j0 + k + 1) << 12]) for k in range(1, m)]
+    raw = [0] + [crc0(mem[(j0 + k) << 12:(j0 + k + 1) << 12]) for k in range(1, m)]  # G' leaves chunk 0 out
     g = 0
     for t in range(nt):
         acc, kk = 0, t
         while kk < m:
-            acc = nib_shift(nt * 4096, acc) ^ raw[kk] ^ (seed if kk == 0 else 0)
+            acc = nib_shift(nt * 4096, acc) ^ raw[kk]
             kk += nt
         if t < m:
             acc = nib_shift(((m - 1 - t) % nt) * 4096, acc)
         g ^= acc
+    g ^= nib_shift((m - 1) * 4096, head ^ seed)  # thread 0 adds the head at the end
     return ~(nib_shift(e - (j1 << 12), g) ^ tail) & 0xFFFFFFFF
-
-
-def test_span_piece_is_crc0():
-    rnd = random.Random(41)
-    mem = rnd.randbytes(3 * 4096 + 8)
-    for ps, pe in [(0, 1), (0, 4096), (5, 4096), (4095, 4096), (4096, 4097), (4097, 8190), (4099, 8195),
-                   (8190, 8192), (6, 7), (3, 4), (4096 + 13, 2 * 4096 + 5)]:
-        assert span_piece_emulated(mem, ps, pe) == crc0(mem[ps:pe]), (ps, pe)
 
 
 @pytest.mark.parametrize("L,start,nt", [
@@ -298,7 +250,7 @@ def test_span_piece_is_crc0():
 ])
 def test_span_fold_matches_zlib(L, start, nt):
     """Span mode: interior blocks from the block table, the partial first / last
-    blocks from the fold's own window pieces -- equal to zlib.crc32 of the body."""
+    blocks from the piece pass -- equal to zlib.crc32 of the body."""
     rnd = random.Random(L * 13 + start)
     mem = bytearray(rnd.randbytes(start + L + 4096))
     assert span_fold_emulated(bytes(mem), start, L, nt) == zlib.crc32(bytes(mem[start:start + L]))

@@ -15,6 +15,8 @@ import rpc_amd  # noqa: E402
 
 DEV = "cuda:0"
 n, L = 1 << 18, 4096
+if os.environ.get("SVC_MAXBLOCKS"):  # persistent-grid cap (a placement test)
+    rpc_amd.set_options(True, int(os.environ["SVC_MAXBLOCKS"]))
 x = torch.empty(n * L, dtype=torch.uint8, device=DEV)
 rpc_amd.fill_random(x, 0x5E7)
 
@@ -34,7 +36,7 @@ def timed(reps=20):
     return float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
 
 
-res = {"lib": os.environ.get("RPCCRC_LIB", "") or "head", "alone_us": round(min(timed() for _ in range(3)), 1)}
+res = {"lib": os.environ.get("RPCCRC_LIB", "") or "head", "max_blocks": os.environ.get("SVC_MAXBLOCKS", "default"), "alone_us": round(min(timed() for _ in range(3)), 1)}
 for blen in [int(a) for a in sys.argv[1:]]:
     body = bytes(range(256)) * 4
     body = body[:blen]
