@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "crc32_layout.h"
+#include "frames.h"
 
 namespace rpccrc {
 
@@ -112,6 +113,10 @@ struct BigRoute {
   const uint32_t *cmp_expected = nullptr;
   const uint8_t *cmp_pre = nullptr;
   uint8_t *cmp_verdict = nullptr;
+  // ... and the aligned plan parses the headers first (parse.frame_off set:
+  // the batch's offsets / lengths are the parse's outputs), so the parse
+  // launch is skipped too.
+  FramesParse parse;
   const uint32_t *dbl = nullptr; // kBigDblWords: the fold's doubling maps per chunk class (build_big_dbl)
 };
 // (The fold's doubling maps per chunk class: crc32_layout.h build_big_dbl.)

@@ -763,46 +763,53 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
     }
     return;
   }
-  uint64_t bytes;
-  if (r.all_n) {
-    unsigned long long x = 0;
-    for (uint64_t b = t; b < nb; b += 1024) x += lengths[b];
-    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
-    if (lane == 0) wsum[w] = x;
-    __syncthreads();
-    bytes = 0;
-    for (uint32_t k = 0; k < 16; ++k) bytes += wsum[k];
-    __syncthreads();
-  } else {
-    bytes = r.meta[1];
-  }
-  if (r.span_rows_max != 0) { // span mode (route-all, base 4 KiB-aligned; BigRoute)
-    // The last body end, and the bytes of the whole blocks inside bodies (the
-    // blocks the fold takes from the span pass).  Dense: the span pass reads at
-    // most 1/16 more than those blocks (+ 1 MiB).
-    unsigned long long hi = 0, inner = 0;
+  // One pass over the bodies (route-all: the routed bytes; span mode: also the
+  // last body end and the bytes of the whole blocks inside bodies, the blocks
+  // the fold takes from the span pass), then one block reduction.  A fused
+  // frames parse (BigRoute.parse) produces each body's offset / length here.
+  unsigned long long x = 0, hi = 0, inner = 0;
+  const bool sums = r.all_n != 0, span = r.span_rows_max != 0;
+  if (sums || r.parse.frame_off != nullptr) {
     for (uint64_t b = t; b < nb; b += 1024) {
-      const uint64_t s0 = offsets[b], L = lengths[b];
-      if (L == 0) continue;
-      const uint64_t e = s0 + L, j0 = s0 >> 12, j1 = (e - 1) >> 12;
-      hi = e > hi ? e : hi;
-      inner += (j1 > j0 + 1) ? (j1 - j0 - 1) << 12 : 0ull;
+      uint64_t s0, L;
+      if (r.parse.frame_off != nullptr) {
+        frames_parse_one(r.parse, b);
+        s0 = r.parse.body_off[b]; // (this thread's own store)
+        L = r.parse.body_len[b];
+      } else {
+        s0 = span ? offsets[b] : 0;
+        L = lengths[b];
+      }
+      x += L;
+      if (span && L != 0) {
+        const uint64_t e = s0 + L, j0 = s0 >> 12, j1 = (e - 1) >> 12;
+        hi = e > hi ? e : hi;
+        inner += (j1 > j0 + 1) ? (j1 - j0 - 1) << 12 : 0ull;
+      }
     }
-    for (int m = 32; m >= 1; m >>= 1) {
-      const unsigned long long h = __shfl_xor(hi, m, 64);
-      hi = h > hi ? h : hi;
-      inner += __shfl_xor(inner, m, 64);
-    }
-    if (lane == 0) wsum[w] = inner;
-    __syncthreads();
-    unsigned long long inner_all = 0;
-    for (uint32_t k = 0; k < 16; ++k) inner_all += wsum[k];
-    __syncthreads();
-    if (lane == 0) wsum[w] = hi;
-    __syncthreads();
-    unsigned long long hi_all = 0;
-    for (uint32_t k = 0; k < 16; ++k) hi_all = wsum[k] > hi_all ? wsum[k] : hi_all;
-    __syncthreads();
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    x += __shfl_xor(x, m, 64);
+    const unsigned long long h = __shfl_xor(hi, m, 64);
+    hi = h > hi ? h : hi;
+    inner += __shfl_xor(inner, m, 64);
+  }
+  __shared__ unsigned long long wred[3][16];
+  if (lane == 0) {
+    wred[0][w] = x;
+    wred[1][w] = hi;
+    wred[2][w] = inner;
+  }
+  __syncthreads(); // (also orders the parse's stores before the chunk scan below reads them)
+  unsigned long long x_all = 0, hi_all = 0, inner_all = 0;
+  for (uint32_t k = 0; k < 16; ++k) {
+    x_all += wred[0][k];
+    hi_all = wred[1][k] > hi_all ? wred[1][k] : hi_all;
+    inner_all += wred[2][k];
+  }
+  const uint64_t bytes = sums ? x_all : r.meta[1];
+  if (span) { // span mode (route-all, base 4 KiB-aligned; BigRoute)
+    // Dense: the span pass reads at most 1/16 more than the interior blocks (+ 1 MiB).
     const uint64_t rows = hi_all >> 12;
     const bool dense = rows <= r.span_rows_max && (rows << 12) <= inner_all + inner_all / 16 + (1ull << 20);
     if (t == 0) {
@@ -1070,7 +1077,7 @@ __global__ void __launch_bounds__(kFoldThreads) big_combine_aligned_kernel(const
 size_t big_route_workspace_bytes(uint64_t n, uint64_t span_rows) {
   return align256((n + 63) / 64 * 8) + align256(64) + align256(kBigMaxBodies * 4) +
          align256((kBigMaxBodies + 1) * 8) + align256(kBigMaxChunks * 8) + 2 * align256(kBigMaxChunks * 4) +
-         align256(span_rows * 4);
+         (span_rows ? align256((span_rows + 1) * 4) : 0);
 }
 
 BigRoute big_route_carve(void *ws, uint64_t n, uint64_t span_rows) {
@@ -1089,7 +1096,7 @@ BigRoute big_route_carve(void *ws, uint64_t n, uint64_t span_rows) {
   r.c_len = reinterpret_cast<uint32_t *>(take(kBigMaxChunks * 4));
   r.c_raw = reinterpret_cast<uint32_t *>(take(kBigMaxChunks * 4));
   if (span_rows) {
-    r.blk = reinterpret_cast<uint32_t *>(take(span_rows * 4));
+    r.blk = reinterpret_cast<uint32_t *>(take((span_rows + 1) * 4)); // (+1: the fold's idle loads read blk[j0])
     r.span_rows_max = span_rows;
   }
   return r;
@@ -1123,7 +1130,7 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
     hipLaunchKernelGGL(big_plan_aligned_kernel, dim3(1), dim3(1024), 0, s, proto.base, proto.offsets, proto.lengths, r);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(big_expand_aligned_kernel, dim3(512), dim3(256), 0, s, proto.base, proto.offsets, proto.lengths,
+    hipLaunchKernelGGL(big_expand_aligned_kernel, dim3(128), dim3(256), 0, s, proto.base, proto.offsets, proto.lengths,
                        r);
   } else {
     // The fold indexes its maps by chunk class: chunk = 4096 * 2^m - 16 (the plan

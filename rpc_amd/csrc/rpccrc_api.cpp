@@ -638,7 +638,8 @@ struct FramesCmp {
 };
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
            uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route, uint32_t *err = nullptr,
-           uint64_t span_bytes = 0, const FramesCmp *cmp = nullptr, bool *compared = nullptr) {
+           uint64_t span_bytes = 0, const FramesCmp *cmp = nullptr, bool *compared = nullptr,
+           const FramesParse *fparse = nullptr) {
   const int path = g_ragged_path.load(std::memory_order_relaxed);
   const bool nt = nontemporal();
   const int mb = max_blocks_for(c);
@@ -651,6 +652,19 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   const bool packed = fits && (path == RPCCRC_RAGGED_PACKED || (auto_frames && !kAutoSplitFrames));
   const bool split = !packed && n <= kMaxLaunchItems && (path == RPCCRC_RAGGED_SPLIT || (auto_frames && kAutoSplitFrames));
   route = route && !packed && mode == kModeFinal && n <= kMaxLaunchItems;
+  // Route-all: a lifted-cap frames batch of at most kRouteAllMax frames sends
+  // every body through the chunk route (no classify pass and no plain rows
+  // pass, whose longest non-routed body -- up to the 16 KiB small-batch
+  // threshold, one wave -- set its duration: 15 us of a 1024-frame verify).
+  // Bounded because the fold spends a block-wide reduction per body (1024
+  // blocks): a few bodies per block cost less than the passes they replace.
+  const bool route_all = route && small_bodies && !split && n <= kRouteAllMax && !g_big_min_env;
+  // fparse (frames verify): the route-all aligned plan parses the headers
+  // itself; any other path needs them parsed before its first launch.
+  const bool fuse_parse = fparse && route_all && g_big_aligned;
+  if (fparse && !fuse_parse)
+    RPCCRC_TRY(launch_frames_parse(fparse->stream, fparse->stream_bytes, fparse->frame_off, n, fparse->flags,
+                                   fparse->body_off, fparse->body_len, fparse->hdr_crc, fparse->pre, s));
   ItemsArgs a = items_args(c, base, offsets, lengths, n, 0, 0, mode, out);
   if (err) a.err = err;
   if (packed) {
@@ -677,13 +691,6 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   size_t split_bytes = 0;
   if (split) RPCCRC_TRY(split_workspace_bytes(n, &split_bytes));
   split_bytes = (split_bytes + 255) & ~(size_t)255;
-  // Route-all: a lifted-cap frames batch of at most kRouteAllMax frames sends
-  // every body through the chunk route (no classify pass and no plain rows
-  // pass, whose longest non-routed body -- up to the 16 KiB small-batch
-  // threshold, one wave -- set its duration: 15 us of a 1024-frame verify).
-  // Bounded because the fold spends a block-wide reduction per body (1024
-  // blocks): a few bodies per block cost less than the passes they replace.
-  const bool route_all = route && small_bodies && !split && n <= kRouteAllMax && !g_big_min_env;
   // Span mode (route-all over a 4 KiB-aligned stream of >= kSpanMinBytes; the
   // plan still falls back to chunks when the bodies are sparse in it).
   const uint64_t span_rows = (route_all && g_big_span && g_big_aligned && ((uintptr_t)base & 4095u) == 0 &&
@@ -712,6 +719,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
         r.cmp_verdict = cmp->verdict;
         if (compared) *compared = true;
       }
+      if (fuse_parse) r.parse = *fparse;
     } else {
       const uint32_t big_min = big_min_for(n);
       RPCCRC_TRY(launch_big_classify(lengths, n, big_min, r, s));
@@ -1404,11 +1412,20 @@ int rpc_frames_verify_device(const uint8_t *d_stream, uint64_t stream_bytes, con
   uint32_t *bexp = reinterpret_cast<uint32_t *>(ws + align256(n * 8) + align256(n * 4));
   uint32_t *bcrc = d_crc ? d_crc : reinterpret_cast<uint32_t *>(ws + align256(n * 8) + 2 * align256(n * 4));
   uint8_t *pre = ws + align256(n * 8) + 3 * align256(n * 4);
-  RPCCRC_TRY(launch_frames_parse(d_stream, stream_bytes, d_frame_offsets, n, flags, boff, blen, bexp, pre, s));
+  FramesParse fp; // (launched by ragged(), or fused into the route's plan)
+  fp.stream = d_stream;
+  fp.stream_bytes = stream_bytes;
+  fp.frame_off = d_frame_offsets;
+  fp.flags = flags;
+  fp.body_off = boff;
+  fp.body_len = blen;
+  fp.hdr_crc = bexp;
+  fp.pre = pre;
   const bool lift = (flags & RPC_FRAMES_LIFT_CAP) != 0;
   const FramesCmp cmp{bexp, pre, d_verdict};
   bool compared = false;
-  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes, &cmp, &compared)))
+  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes, &cmp, &compared,
+                   &fp)))
     return rc;
   if (compared) return RPCCRC_OK; // (route-all: the fold wrote the verdicts)
   return map_hip(launch_frames_compare(bcrc, bexp, pre, n, d_verdict, s));
