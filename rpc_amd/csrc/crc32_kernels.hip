@@ -218,14 +218,19 @@ __global__ void __launch_bounds__(1024, 4) stream_read_kernel(const uint4 *p, ui
 static constexpr int kBlock = 1024;
 
 // Fraction of a launch's rounds dealt from the steal pool (RPCCRC_STEAL_FRAC,
-// 0 disables stealing).
-static double steal_frac() {
-  static const double f = [] {
-    const char *e = getenv("RPCCRC_STEAL_FRAC");
-    const double v = e ? atof(e) : 0.15; // NS: 0.08 / 0.15 / 0.25 -> -3.9 / -4.3 / -3.2 % (r02w)
-    return (v >= 0.0 && v < 1.0) ? v : 0.15;
-  }();
-  return f;
+// 0 disables stealing; NS r02w: 0.08 / 0.15 / 0.25 -> -3.9 / -4.3 / -3.2 %).
+// QB = 4 launches (C1) may take their own (RPCCRC_STEAL_FRAC_QB4): 0.08 and
+// 0.15 measured the same on C1 with the run order rotated (0.25 +1.3 %;
+// profiles/r04k/c1_steal_ab.txt, ab2).
+static double env_frac(const char *name, double dflt) {
+  const char *e = getenv(name);
+  const double v = e ? atof(e) : dflt;
+  return (v >= 0.0 && v < 1.0) ? v : dflt;
+}
+static double steal_frac(int QB = 1) {
+  static const double f1 = env_frac("RPCCRC_STEAL_FRAC", 0.15);
+  static const double f4 = env_frac("RPCCRC_STEAL_FRAC_QB4", f1);
+  return QB == 4 ? f4 : f1;
 }
 
 hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream, hipEvent_t steal_done,
@@ -269,10 +274,10 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // rounds go to the device-counter pool, the rest stay static per workgroup.
   ItemsArgs k = a;
   k.steal_s = 0;
-  k.steal_permille = (uint32_t)(steal_frac() * 1000.0 + 0.5);
+  k.steal_permille = (uint32_t)(steal_frac(QB) * 1000.0 + 0.5);
   if (dyn && a.steal != nullptr && a.n_dev == nullptr) {
     const uint64_t rounds = (n_tasks + round - 1) / round;
-    const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac())) / blocks;
+    const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac(QB))) / blocks;
     if (st >= kStealAhead && st * blocks < rounds) k.steal_s = (uint32_t)st;
   } else if (dyn && a.steal != nullptr && k.steal_permille > 0) {
     k.steal_s = kStealOnDevice; // device-counted: the kernel sizes the pool from *n_dev

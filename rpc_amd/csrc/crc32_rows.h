@@ -631,8 +631,11 @@ constexpr bool kRowsMetaReuse = RPCCRC_META_REUSE != 0;
 #endif
 constexpr bool kRaggedAhead2 = RPCCRC_RAGGED_AHEAD2 != 0;
 // First row's loads issued under the LDS image copy (crc32_rows_kernel kEarly).
+// On since round 4: with the compact image (33 KiB read per workgroup) the
+// overlap pays -- rotated-order A/B on one box: NS -0.5 %, C1 -0.6 %, C4
+// -0.25 %, C2 -0.1 % (profiles/r04k/ab2, ab3); round 3 (155 KiB image): +-1 %.
 #ifndef RPCCRC_EARLY_ROW
-#define RPCCRC_EARLY_ROW 0
+#define RPCCRC_EARLY_ROW 1
 #endif
 constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
 #ifndef RPCCRC_STEAL_EXIT_ACQREL

@@ -8,9 +8,14 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1; LIBS=$2; CFGS=$3; ROUNDS=${4:-2}
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+# the library order rotates by one each round (a run's position in a round
+# shifts its result: the first run after a config switch ran slowest, r04k)
+read -r -a LIBARR <<< "$LIBS"
+NL=${#LIBARR[@]}
 for i in $(seq 1 "$ROUNDS"); do
   for c in $CFGS; do
-    for l in $LIBS; do
+    for j in $(seq 0 $((NL - 1))); do
+      l=${LIBARR[$(( (j + i - 1) % NL ))]}
       lib=${l%%:*}; envs=""; [ "$lib" != "$l" ] && envs=$(echo "${l#*:}" | tr ',' ' ')
       if [ "$lib" = head ]; then unset RPCCRC_LIB; else export RPCCRC_LIB=$PWD/abtest/$lib.so; fi
       cfg=${c%%:*}; extra=""; [ "$cfg" != "$c" ] && extra=$(echo "${c#*:}" | tr ',' ' ')
