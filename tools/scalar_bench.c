@@ -94,8 +94,18 @@ int main(int argc, char **argv) {
     if (len == 68) memcpy(body, req, 68);
     const uint32_t want = rpc_crc32(body, len); // warms the device context
     if (ref && ref(body, len) != want) fail = 1;
-    const int tcounts[2] = {1, 10};
-    for (int ti = 0; ti < 2; ++ti) {
+    // SCALAR_BENCH_THREADS="1,2,4,..." replaces the thread counts (a probe of
+    // how the drop-in scales; the default rows are the reference's 1 and 10).
+    int tcounts[16] = {1, 10}, nt = 2;
+    if (getenv("SCALAR_BENCH_THREADS")) {
+      nt = 0;
+      for (char *p = getenv("SCALAR_BENCH_THREADS"); *p && nt < 16;) {
+        tcounts[nt++] = (int)strtol(p, &p, 10);
+        if (*p == ',') ++p;
+        else break;
+      }
+    }
+    for (int ti = 0; ti < nt; ++ti) {
       const int th = tcounts[ti];
       double us, cps, rus = -1, rcps = -1;
       long bad, rbad = 0;
