@@ -117,6 +117,9 @@ struct BigRoute {
   // the batch's offsets / lengths are the parse's outputs), so the parse
   // launch is skipped too.
   FramesParse parse;
+  // Frames stamp in route-all mode: the plan runs the stamp's bounds / cap
+  // check (stamp.frame_off set), and the fold writes each OK frame's header.
+  FramesStamp stamp;
   const uint32_t *dbl = nullptr; // kBigDblWords: the fold's doubling maps per chunk class (build_big_dbl)
 };
 // (The fold's doubling maps per chunk class: crc32_layout.h build_big_dbl.)

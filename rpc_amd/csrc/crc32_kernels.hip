@@ -771,16 +771,21 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
   // One pass over the bodies (route-all: the routed bytes; span mode: also the
   // last body end and the bytes of the whole blocks inside bodies, the blocks
   // the fold takes from the span pass), then one block reduction.  A fused
-  // frames parse (BigRoute.parse) produces each body's offset / length here.
+  // frames parse or stamp check (BigRoute.parse / .stamp) produces each body's
+  // offset / length here.
   unsigned long long x = 0, hi = 0, inner = 0;
   const bool sums = r.all_n != 0, span = r.span_rows_max != 0;
-  if (sums || r.parse.frame_off != nullptr) {
+  if (sums || r.parse.frame_off != nullptr || r.stamp.frame_off != nullptr) {
     for (uint64_t b = t; b < nb; b += 1024) {
       uint64_t s0, L;
       if (r.parse.frame_off != nullptr) {
         frames_parse_one(r.parse, b);
         s0 = r.parse.body_off[b]; // (this thread's own store)
         L = r.parse.body_len[b];
+      } else if (r.stamp.frame_off != nullptr) {
+        frames_stamp_prep_one(r.stamp, b);
+        s0 = r.stamp.body_off[b];
+        L = r.stamp.len_eff[b];
       } else {
         s0 = span ? offsets[b] : 0;
         L = lengths[b];
@@ -1029,6 +1034,7 @@ __global__ void __launch_bounds__(kFoldThreads) big_combine_aligned_kernel(const
       }
       out[i] = crc; // an empty body: crc32 = 0
       if (r.cmp_verdict) fold_verdict(r, i, crc);
+      if (r.stamp.frame_off) frames_stamp_one(r.stamp, i, crc);
     }
     __syncthreads();
   }
@@ -1072,6 +1078,7 @@ __global__ void __launch_bounds__(kFoldThreads) big_combine_aligned_kernel(const
       }
       out[i] = crc; // an empty body: crc32 = 0
       if (r.cmp_verdict) fold_verdict(r, i, crc);
+      if (r.stamp.frame_off) frames_stamp_one(r.stamp, i, crc);
     }
     __syncthreads();
   }

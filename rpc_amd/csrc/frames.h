@@ -76,19 +76,62 @@ __device__ __forceinline__ void frames_parse_one(const FramesParse &p, uint64_t 
 // applies the reference's type / cap / bounds rules (frames.hip): the body
 // offset and effective length (0 when the body is not read), the header crc32
 // and the verdict so far (RPC_FRAME_* or kFramePending).
+// The stamp side of a call: frame i's body offset / effective length and its
+// verdict (the bounds and the cap, rpc_async.c:499-501), then the 12-byte
+// big-endian header of every OK frame (rpc_async.c:521-530: htons / htonl).
+struct FramesStamp {
+  uint8_t *stream = nullptr;
+  uint64_t stream_bytes = 0;
+  const uint64_t *frame_off = nullptr; // nullptr: no stamp requested
+  const uint32_t *body_len = nullptr;
+  int flags = 0;
+  uint16_t version = 0, type = 0;
+  uint64_t *body_off = nullptr;
+  uint32_t *len_eff = nullptr;
+  uint8_t *pre = nullptr; // the verdict: OK (stamped), TOO_LARGE or MALFORMED
+};
+__device__ __forceinline__ void frames_stamp_prep_one(const FramesStamp &p, uint64_t i) {
+  const uint64_t off = p.frame_off[i];
+  const uint32_t bl = p.body_len[i];
+  uint8_t v = RPC_FRAME_OK;
+  if (!inside(off, kFrameHeaderLen, p.stream_bytes) || !inside(off + kFrameHeaderLen, bl, p.stream_bytes))
+    v = RPC_FRAME_MALFORMED;
+  else if (bl > RPC_MAX_BODY_LEN && !(p.flags & RPC_FRAMES_LIFT_CAP))
+    v = RPC_FRAME_TOO_LARGE;
+  p.body_off[i] = (v == RPC_FRAME_OK) ? off + kFrameHeaderLen : 0;
+  p.len_eff[i] = (v == RPC_FRAME_OK) ? bl : 0u;
+  p.pre[i] = v;
+}
+__device__ __forceinline__ void put_be16(uint8_t *p, uint16_t v) {
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)v;
+}
+__device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24);
+  p[1] = (uint8_t)(v >> 16);
+  p[2] = (uint8_t)(v >> 8);
+  p[3] = (uint8_t)v;
+}
+// (only header bytes are written: no body's CRC depends on them)
+__device__ __forceinline__ void frames_stamp_one(const FramesStamp &p, uint64_t i, uint32_t crc) {
+  if (p.pre[i] != RPC_FRAME_OK) return;
+  uint8_t *h = p.stream + p.frame_off[i];
+  put_be16(h + 0, p.version);
+  put_be16(h + 2, p.type);
+  put_be32(h + 4, p.body_len[i]);
+  put_be32(h + 8, crc);
+}
+
 hipError_t launch_frames_parse(const uint8_t *stream, uint64_t stream_bytes, const uint64_t *frame_off, uint64_t n,
                                int flags, uint64_t *body_off, uint32_t *body_len, uint32_t *hdr_crc, uint8_t *pre,
                                hipStream_t s);
 // verdict[i] = pre[i], or for pending data frames OK / BAD_CRC by crc == expected.
 hipError_t launch_frames_compare(const uint32_t *crc, const uint32_t *expected, const uint8_t *pre, uint64_t n,
                                  uint8_t *verdict, hipStream_t s);
-// Stamp side: bounds + cap (rpc_async.c:499-501) -> body offset, effective length, OK / TOO_LARGE / MALFORMED.
-hipError_t launch_frames_stamp_prep(uint64_t stream_bytes, const uint64_t *frame_off, const uint32_t *body_len,
-                                    uint64_t n, int flags, uint64_t *body_off, uint32_t *len_eff, uint8_t *pre,
-                                    hipStream_t s);
-// Writes the header of every OK frame as rpc_async.c:521-530 does (htons/htonl + memcpy).
-hipError_t launch_frames_stamp(uint8_t *stream, const uint64_t *frame_off, const uint32_t *body_len,
-                               const uint32_t *crc, const uint8_t *pre, uint64_t n, uint16_t version, uint16_t type,
-                               hipStream_t s);
+// Stamp side: bounds + cap (rpc_async.c:499-501) -> body offset, effective
+// length, OK / TOO_LARGE / MALFORMED (frames_stamp_prep_one); then the header of
+// every OK frame (frames_stamp_one).
+hipError_t launch_frames_stamp_prep(const FramesStamp &p, uint64_t n, hipStream_t s);
+hipError_t launch_frames_stamp(const FramesStamp &p, const uint32_t *crc, uint64_t n, hipStream_t s);
 
 } // namespace rpccrc

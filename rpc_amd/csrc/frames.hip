@@ -8,17 +8,6 @@
 namespace rpccrc {
 
 namespace {
-__device__ __forceinline__ void put_be16(uint8_t *p, uint16_t v) {
-  p[0] = (uint8_t)(v >> 8);
-  p[1] = (uint8_t)v;
-}
-__device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v) {
-  p[0] = (uint8_t)(v >> 24);
-  p[1] = (uint8_t)(v >> 16);
-  p[2] = (uint8_t)(v >> 8);
-  p[3] = (uint8_t)v;
-}
-
 // (the rule: frames.h frames_parse_one)
 __global__ void frames_parse_kernel(FramesParse p, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -33,34 +22,14 @@ __global__ void frames_compare_kernel(const uint32_t *crc, const uint32_t *expec
   verdict[i] = (p != kFramePending) ? p : (crc[i] == expected[i] ? RPC_FRAME_OK : RPC_FRAME_BAD_CRC);
 }
 
-// Stamp side: the body of frame i must lie inside the stream, and without
-// LIFT_CAP be at most MAX_BODY_LEN (rpc_async.c:499-501 refuses to send it).
-__global__ void frames_stamp_prep_kernel(uint64_t stream_bytes, const uint64_t *frame_off, const uint32_t *body_len,
-                                         uint64_t n, int flags, uint64_t *body_off, uint32_t *len_eff, uint8_t *pre) {
+// Stamp side (the rules: frames.h frames_stamp_prep_one / frames_stamp_one).
+__global__ void frames_stamp_prep_kernel(FramesStamp p, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t off = frame_off[i];
-  const uint32_t bl = body_len[i];
-  uint8_t v = RPC_FRAME_OK;
-  if (!inside(off, kFrameHeaderLen, stream_bytes) || !inside(off + kFrameHeaderLen, bl, stream_bytes))
-    v = RPC_FRAME_MALFORMED;
-  else if (bl > RPC_MAX_BODY_LEN && !(flags & RPC_FRAMES_LIFT_CAP))
-    v = RPC_FRAME_TOO_LARGE;
-  body_off[i] = (v == RPC_FRAME_OK) ? off + kFrameHeaderLen : 0;
-  len_eff[i] = (v == RPC_FRAME_OK) ? bl : 0u;
-  pre[i] = v;
+  if (i < n) frames_stamp_prep_one(p, i);
 }
-
-__global__ void frames_stamp_kernel(uint8_t *stream, const uint64_t *frame_off, const uint32_t *body_len,
-                                    const uint32_t *crc, const uint8_t *pre, uint64_t n, uint16_t version,
-                                    uint16_t type) {
+__global__ void frames_stamp_kernel(FramesStamp p, const uint32_t *crc, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || pre[i] != RPC_FRAME_OK) return;
-  uint8_t *h = stream + frame_off[i];
-  put_be16(h + 0, version);
-  put_be16(h + 2, type);
-  put_be32(h + 4, body_len[i]);
-  put_be32(h + 8, crc[i]);
+  if (i < n) frames_stamp_one(p, i, crc[i]);
 }
 
 dim3 grid_for(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
@@ -88,19 +57,13 @@ hipError_t launch_frames_compare(const uint32_t *crc, const uint32_t *expected, 
   return hipGetLastError();
 }
 
-hipError_t launch_frames_stamp_prep(uint64_t stream_bytes, const uint64_t *frame_off, const uint32_t *body_len,
-                                    uint64_t n, int flags, uint64_t *body_off, uint32_t *len_eff, uint8_t *pre,
-                                    hipStream_t s) {
-  hipLaunchKernelGGL(frames_stamp_prep_kernel, grid_for(n), dim3(256), 0, s, stream_bytes, frame_off, body_len, n,
-                     flags, body_off, len_eff, pre);
+hipError_t launch_frames_stamp_prep(const FramesStamp &p, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(frames_stamp_prep_kernel, grid_for(n), dim3(256), 0, s, p, n);
   return hipGetLastError();
 }
 
-hipError_t launch_frames_stamp(uint8_t *stream, const uint64_t *frame_off, const uint32_t *body_len,
-                               const uint32_t *crc, const uint8_t *pre, uint64_t n, uint16_t version, uint16_t type,
-                               hipStream_t s) {
-  hipLaunchKernelGGL(frames_stamp_kernel, grid_for(n), dim3(256), 0, s, stream, frame_off, body_len, crc, pre, n,
-                     version, type);
+hipError_t launch_frames_stamp(const FramesStamp &p, const uint32_t *crc, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(frames_stamp_kernel, grid_for(n), dim3(256), 0, s, p, crc, n);
   return hipGetLastError();
 }
 

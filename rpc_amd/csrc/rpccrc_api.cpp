@@ -639,7 +639,7 @@ struct FramesCmp {
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
            uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route, uint32_t *err = nullptr,
            uint64_t span_bytes = 0, const FramesCmp *cmp = nullptr, bool *compared = nullptr,
-           const FramesParse *fparse = nullptr) {
+           const FramesParse *fparse = nullptr, const FramesStamp *fstamp = nullptr, bool *stamped = nullptr) {
   const int path = g_ragged_path.load(std::memory_order_relaxed);
   const bool nt = nontemporal();
   const int mb = max_blocks_for(c);
@@ -665,6 +665,10 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   if (fparse && !fuse_parse)
     RPCCRC_TRY(launch_frames_parse(fparse->stream, fparse->stream_bytes, fparse->frame_off, n, fparse->flags,
                                    fparse->body_off, fparse->body_len, fparse->hdr_crc, fparse->pre, s));
+  // fstamp (frames stamp): likewise the stamp's bounds / cap check, and the fold
+  // then writes the headers (*stamped set; the caller skips its stamp launch).
+  const bool fuse_stamp = fstamp && route_all && g_big_aligned;
+  if (fstamp && !fuse_stamp) RPCCRC_TRY(launch_frames_stamp_prep(*fstamp, n, s));
   ItemsArgs a = items_args(c, base, offsets, lengths, n, 0, 0, mode, out);
   if (err) a.err = err;
   if (packed) {
@@ -720,6 +724,10 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
         if (compared) *compared = true;
       }
       if (fuse_parse) r.parse = *fparse;
+      if (fuse_stamp) {
+        r.stamp = *fstamp;
+        if (stamped) *stamped = true;
+      }
     } else {
       const uint32_t big_min = big_min_for(n);
       RPCCRC_TRY(launch_big_classify(lengths, n, big_min, r, s));
@@ -1449,10 +1457,24 @@ int rpc_frames_stamp_device(uint8_t *d_stream, uint64_t stream_bytes, const uint
   uint32_t *blen = reinterpret_cast<uint32_t *>(ws + align256(n * 8));
   uint32_t *bcrc = reinterpret_cast<uint32_t *>(ws + align256(n * 8) + align256(n * 4));
   uint8_t *pre = d_verdict ? d_verdict : ws + align256(n * 8) + 2 * align256(n * 4);
-  RPCCRC_TRY(launch_frames_stamp_prep(stream_bytes, d_frame_offsets, d_body_lens, n, flags, boff, blen, pre, s));
+  FramesStamp st; // (the check launched by ragged(), or fused into the route's plan; the headers likewise)
+  st.stream = d_stream;
+  st.stream_bytes = stream_bytes;
+  st.frame_off = d_frame_offsets;
+  st.body_len = d_body_lens;
+  st.flags = flags;
+  st.version = version;
+  st.type = type;
+  st.body_off = boff;
+  st.len_eff = blen;
+  st.pre = pre;
   const bool lift = (flags & RPC_FRAMES_LIFT_CAP) != 0;
-  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes))) return rc;
-  return map_hip(launch_frames_stamp(d_stream, d_frame_offsets, d_body_lens, bcrc, pre, n, version, type, s));
+  bool stamped = false;
+  if ((rc = ragged(*c, d_stream, boff, blen, n, kModeFinal, bcrc, s, true, lift, nullptr, stream_bytes, nullptr,
+                   nullptr, nullptr, &st, &stamped)))
+    return rc;
+  if (stamped) return RPCCRC_OK; // (route-all: the fold wrote the headers)
+  return map_hip(launch_frames_stamp(st, bcrc, n, s));
 }
 
 uint32_t rpc_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) { return crc32_combine(crc1, crc2, len2); }
