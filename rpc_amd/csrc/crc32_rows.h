@@ -645,6 +645,13 @@ constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
 #define RPCCRC_STEAL_AHEAD 1
 #endif
 constexpr uint32_t kStealAhead = RPCCRC_STEAL_AHEAD;
+// The task of a local round whose taker issues the claim (0: the round's first).
+// A later task commits less work ahead of the pool's end (the drain) but leaves
+// the claim less time to return before the next round needs it.
+#ifndef RPCCRC_STEAL_CLAIM_AT
+#define RPCCRC_STEAL_CLAIM_AT 0
+#endif
+constexpr uint32_t kStealClaimAt = RPCCRC_STEAL_CLAIM_AT;
 constexpr uint32_t kStealQ = 16;                      // LDS queue ring
 constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
 // Bounded waits.  Both waits end by protocol (a claim is published by the wave
@@ -859,7 +866,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // The wave taking local round r's first task claims a pool round for the
   // workgroup (for use kStealAhead rounds later).
   auto claim_if_first = [&](uint32_t c) { // uniform
-    if (!steal || c % kRound != 0u || c / kRound + kStealAhead < steal_s) return;
+    if (!steal || c % kRound != kStealClaimAt || c / kRound + kStealAhead < steal_s) return;
     publish(); // at most one claim in flight per wave
     uint32_t go = 0;
     if (lane == 0 && lds_ld_acq(q_done) == 0u) {
