@@ -773,7 +773,7 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
   // the fold takes from the span pass), then one block reduction.  A fused
   // frames parse or stamp check (BigRoute.parse / .stamp) produces each body's
   // offset / length here.
-  unsigned long long x = 0, hi = 0, inner = 0;
+  unsigned long long x = 0, hi = 0, inner = 0, disorder = 0;
   const bool sums = r.all_n != 0, span = r.span_rows_max != 0;
   if (sums || r.parse.frame_off != nullptr || r.stamp.frame_off != nullptr) {
     for (uint64_t b = t; b < nb; b += 1024) {
@@ -786,6 +786,10 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
         frames_stamp_prep_one(r.stamp, b);
         s0 = r.stamp.body_off[b];
         L = r.stamp.len_eff[b];
+        // Span mode's fold reads the partial blocks while it writes headers:
+        // only frames in stream order, none overlapping the next, keep every
+        // header out of every body (else the chunk route: all CRCs first).
+        if (b + 1 < nb && r.stamp.frame_off[b] + kFrameHeaderLen + L > r.stamp.frame_off[b + 1]) disorder = 1;
       } else {
         s0 = span ? offsets[b] : 0;
         L = lengths[b];
@@ -803,25 +807,29 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
     const unsigned long long h = __shfl_xor(hi, m, 64);
     hi = h > hi ? h : hi;
     inner += __shfl_xor(inner, m, 64);
+    disorder |= __shfl_xor(disorder, m, 64);
   }
-  __shared__ unsigned long long wred[3][16];
+  __shared__ unsigned long long wred[4][16];
   if (lane == 0) {
     wred[0][w] = x;
     wred[1][w] = hi;
     wred[2][w] = inner;
+    wred[3][w] = disorder;
   }
   __syncthreads(); // (also orders the parse's stores before the chunk scan below reads them)
-  unsigned long long x_all = 0, hi_all = 0, inner_all = 0;
+  unsigned long long x_all = 0, hi_all = 0, inner_all = 0, disorder_all = 0;
   for (uint32_t k = 0; k < 16; ++k) {
     x_all += wred[0][k];
     hi_all = wred[1][k] > hi_all ? wred[1][k] : hi_all;
     inner_all += wred[2][k];
+    disorder_all |= wred[3][k];
   }
   const uint64_t bytes = sums ? x_all : r.meta[1];
   if (span) { // span mode (route-all, base 4 KiB-aligned; BigRoute)
     // Dense: the span pass reads at most 1/16 more than the interior blocks (+ 1 MiB).
     const uint64_t rows = hi_all >> 12;
-    const bool dense = rows <= r.span_rows_max && (rows << 12) <= inner_all + inner_all / 16 + (1ull << 20);
+    const bool dense =
+        rows <= r.span_rows_max && (rows << 12) <= inner_all + inner_all / 16 + (1ull << 20) && disorder_all == 0;
     if (t == 0) {
       r.meta[4] = dense ? rows : 0;
       r.meta[5] = dense ? 1 : 0;

@@ -320,6 +320,35 @@ def test_frames_lifted_cap_span_mode(sparse):
     assert all(v[i] == rpc_amd.FRAME_BAD_CRC for i in flips)
 
 
+def test_frames_lifted_cap_stamp_unordered_frames():
+    """Lifted-cap stamp over a 4 KiB-aligned dense stream whose frame offsets are
+    given in reverse order: the route's span mode is
+    for frames in stream order only (its fold reads partial blocks while it
+    writes headers), so these take the chunk route -- every header still equals
+    the oracle's, computed over the bytes before any header is written."""
+    rng = np.random.default_rng(31)
+    lens = [5000, 70000, 1 << 20, 3, 4096 - HDR, 200000, 12345, 0, 90000]
+    sizes = [HDR + L for L in lens]
+    total = sum(sizes)
+    base = aligned_stream(total)
+    fill = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(fill, 0x77AA)
+    base.copy_(fill[:total])
+    offs = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
+    before = base.cpu().numpy().copy()
+    order = np.arange(len(lens))[::-1].copy()
+    do = to_dev(offs[order].view(np.int64))
+    dl = to_dev(np.array([lens[i] for i in order], dtype=np.uint32).view(np.int32))
+    sv = rpc_amd.frames_stamp(base, do, dl, lift_cap=True, stream_bytes=total)
+    assert sv.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(lens)
+    host = base.cpu().numpy()
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        o = int(o)
+        want = oracle.crc32(before[o + HDR:o + HDR + L])
+        assert host[o:o + HDR].tobytes() == header(L, want), i
+        assert host[o + HDR:o + HDR + L].tobytes() == before[o + HDR:o + HDR + L].tobytes()
+
+
 def test_frames_role_flags_rejected():
     d = to_dev(np.zeros(64, dtype=np.uint8))
     o = to_dev(np.zeros(1, dtype=np.int64))
