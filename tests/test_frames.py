@@ -320,6 +320,34 @@ def test_frames_lifted_cap_span_mode(sparse):
     assert all(v[i] == rpc_amd.FRAME_BAD_CRC for i in flips)
 
 
+@pytest.mark.parametrize("role", ["server", "client"])
+def test_frames_lifted_cap_span_mode_verdicts(role):
+    """Span mode (4 KiB-aligned dense stream of >= 1 MiB) with every verdict the
+    parse decides: heartbeats of both types, empty bodies, a bad CRC, a header
+    whose length runs past the stream, and the last body ending exactly at a
+    stream end that is not a multiple of 4 KiB (its last block is partial, so no
+    span-pass block covers it)."""
+    rng = np.random.default_rng(41 if role == "server" else 42)
+    frames = []
+    for L in [300000, 0, 4096 - HDR, 1 << 20, 17, 8192, 0, 65536 + 5]:
+        b = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        frames.append(header(L, oracle.crc32(np.frombuffer(b, dtype=np.uint8)) if L else 0) + b)
+    frames.append(header(0, 0, type_=rpc_amd.RPC_TYPE_PING))
+    frames.append(header(5, 123, type_=rpc_amd.RPC_TYPE_PONG) + b"abcde")
+    b = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    frames.append(header(70000, oracle.crc32(np.frombuffer(b, dtype=np.uint8)) ^ 1) + b)  # bad CRC
+    frames.append(header(1 << 22, 7) + b"short")  # runs past the stream
+    b = rng.integers(0, 256, 123457, dtype=np.uint8).tobytes()
+    frames.append(header(123457, oracle.crc32(np.frombuffer(b, dtype=np.uint8))) + b)  # ends the stream
+    blob, offs = layout(frames)  # (the 4 MiB length of the short frame runs past this ~1.7 MiB stream)
+    assert len(blob) % 4096 != 0 and len(blob) >= (1 << 20)
+    base = aligned_stream(len(blob))
+    base.copy_(torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()).to(DEV))
+    v, c = rpc_amd.frames_verify(base, to_dev(offs.view(np.int64)), role=role, lift_cap=True, stream_bytes=len(blob))
+    want = expected(blob, offs, role=role, lift_cap=True)
+    assert (v.cpu().numpy().tolist(), u32(c).tolist()) == want
+
+
 def test_frames_lifted_cap_stamp_unordered_frames():
     """Lifted-cap stamp over a 4 KiB-aligned dense stream whose frame offsets are
     given in reverse order: the route's span mode is
