@@ -47,6 +47,10 @@ struct ItemsArgs {
   // combine XORs into them afterwards).
   uint32_t *zero_out = nullptr;
   uint32_t zero_n = 0;
+  // Round values (uniform QB = 1 DYN launches of 4096-byte RAW items whose
+  // lds_image carries the round maps, crc32_rows.h kRowsRoundOut): crc0 of
+  // round r's 32 items at round_out[r].  launch_rows refuses it otherwise.
+  uint32_t *round_out = nullptr;
   // Device error word of the launch's device (pinned host memory, zero while
   // all is well).  A wave whose bounded wait in the DYN / tail-stealing
   // protocol runs out stores kErr* into it (crc32_rows.h); the host turns a

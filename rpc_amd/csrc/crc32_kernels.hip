@@ -130,6 +130,8 @@ __global__ void __launch_bounds__(NT) crc32_chunk_combine_kernel(CombineArgs a) 
 // pass zeroed (ItemsArgs.zero_out).  The combine is bound by LDS lookups (8
 // per map): one block per body (16 CUs for C4) took 21-23 us at 4 KiB
 // chunks, 16 blocks per body spread it over the chip (profiles/r02/r02ab_*).
+// Round values (ItemsArgs.round_out: one crc0 per 128 KiB, chunk = 131072):
+// 128 * S values per body, one block per body, the threads past them idle.
 __global__ void __launch_bounds__(1024) crc32_chunk_combine_contig_kernel(CombineArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t nib[kShiftNibWords];
   __shared__ uint32_t part[16];
@@ -137,10 +139,11 @@ __global__ void __launch_bounds__(1024) crc32_chunk_combine_contig_kernel(Combin
   const uint32_t s = blockIdx.x % a.splits;
   const uint32_t t = threadIdx.x;
   const uint64_t L = a.inline_bodies ? a.bodies.b[b].len : a.lengths[b];
-  const uint64_t first = a.inline_bodies ? a.bodies.b[b].chunk_first : a.chunk_first[b];
-  const uint64_t nch = L / a.chunk;                       // 4096 * splits
+  const uint64_t nch = L / a.chunk;                       // 4096 * splits (round values: 128 * S, splits = 1)
+  const uint64_t first = b * nch;                         // equal bodies back to back
   const uint64_t k0 = 4ull * ((uint64_t)s * 1024u + t); // this thread's first chunk
-  const uint4 v = *reinterpret_cast<const uint4 *>(a.raw + first + k0);
+  const bool live = k0 < nch;
+  const uint4 v = live ? *reinterpret_cast<const uint4 *>(a.raw + first + k0) : make_uint4(0u, 0u, 0u, 0u);
   {
     uint4 *dst = reinterpret_cast<uint4 *>(nib);
 #pragma unroll
@@ -149,7 +152,7 @@ __global__ void __launch_bounds__(1024) crc32_chunk_combine_contig_kernel(Combin
   __syncthreads();
   const uint32_t ks = (uint32_t)__builtin_ctzll(a.chunk); // A_chunk = one nibble map
   uint32_t acc = nib_apply(nib, ks, nib_apply(nib, ks, nib_apply(nib, ks, v.x) ^ v.y) ^ v.z) ^ v.w;
-  acc = nib_shift(nib, (nch - k0 - 4) * a.chunk, acc);
+  acc = nib_shift(nib, live ? (nch - k0 - 4) * a.chunk : 0ull, acc);
   for (int m = 1; m < 64; m <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, m, 64);
   if ((t & 63u) == 0) part[t >> 6] = acc;
   __syncthreads();
@@ -239,7 +242,8 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // The kernel indexes items and tasks in 32 bits: launches of at most
   // kMaxLaunchItems (a multiple of 4: QB = 4 groups never straddle launches).
   if (a.n_items > kMaxLaunchItems) {
-    if (a.n_dev != nullptr || a.out_idx != nullptr || a.routed != nullptr) return hipErrorInvalidValue;
+    if (a.n_dev != nullptr || a.out_idx != nullptr || a.routed != nullptr || a.round_out != nullptr)
+      return hipErrorInvalidValue;
     for (uint64_t s0 = 0; s0 < a.n_items; s0 += kMaxLaunchItems) {
       ItemsArgs b = a;
       b.n_items = std::min<uint64_t>(kMaxLaunchItems, a.n_items - s0);
@@ -283,6 +287,26 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
     k.steal_s = kStealOnDevice; // device-counted: the kernel sizes the pool from *n_dev
   }
   if (k.steal_s == 0) k.steal = nullptr;
+  if (a.round_out != nullptr) { // kRowsRoundOut: whole DYN rounds of 4096-byte uniform RAW items
+    if (QB != 1 || ragged || !dyn || a.len != 4096 || a.stride != 4096 || a.mode != kModeRaw || a.n_dev != nullptr ||
+        a.out_idx != nullptr || (reinterpret_cast<uintptr_t>(a.base) & 15u) != 0)
+      return hipErrorInvalidValue;
+#define RPCCRC_ROWS_ROUND(N)                                                                                      \
+  do {                                                                                                            \
+    if (k.steal_s && steal_done) {                                                                                \
+      hipExtLaunchKernelGGL((crc32_rows_kernel<1, N, false, kRowsRoundOut, 1, true, true>), grid, block, 0, stream, \
+                            nullptr, steal_done, 0, k);                                                           \
+      if (steal_recorded) *steal_recorded = true;                                                                 \
+    } else if (k.steal_s) {                                                                                       \
+      hipLaunchKernelGGL((crc32_rows_kernel<1, N, false, kRowsRoundOut, 1, true, true>), grid, block, 0, stream, k); \
+    } else {                                                                                                      \
+      hipLaunchKernelGGL((crc32_rows_kernel<1, N, false, kRowsRoundOut, 1, true>), grid, block, 0, stream, k);    \
+    }                                                                                                             \
+  } while (0)
+    if (nt) RPCCRC_ROWS_ROUND(true); else RPCCRC_ROWS_ROUND(false);
+#undef RPCCRC_ROWS_ROUND
+    return hipGetLastError();
+  }
 #define RPCCRC_ROWS(Q, N, R)                                                                      \
   do {                                                                                            \
     if (dyn && k.steal_s) {                                                                       \

@@ -56,6 +56,10 @@ constexpr uint32_t kLdsZI2 = kLdsRW2 + 512;   // 150016
 // TQ16[k] = A_{16k}(0xFFFFFFFF), k = 0..256: zlib pre-conditioning seeds for
 // first rows of 16k bytes (other lengths: round up, undo with ZI).
 constexpr uint32_t kLdsTQ16 = kLdsZI2 + 15 * 512; // 157696
+// kRowsRoundOut launches (crc32_rows.h): A_{4096 * 2^l}, l = 1..4, in [n][nib]
+// layout over ZI[11..14] (pads z = 12..15, which 16-B aligned 4096-byte items never have).
+constexpr uint32_t kLdsRoundMaps = kLdsZI2 + 11 * 512;
+static_assert(kLdsRoundMaps % 256 == 0 && kLdsRoundMaps + 4 * 512 <= kLdsTQ16, "round maps inside ZI");
 // A zero dword (TQ16's 12-byte tail pad): lanes with nothing to look up read it.
 constexpr uint32_t kLdsZero = kLdsTQ16 + 1028;
 static_assert(kLdsTQ16 + 1040 == kLdsBytesV2, "rows image size");

@@ -394,6 +394,14 @@ constexpr int kRowsAblNtStore = 2048; // non-temporal CRC stores (DYN paths; exa
 // the instruction cost of a half-width row (timing only: wrong CRCs).
 constexpr int kRowsAblHalfChain = 8192;
 constexpr int kRowsAblNoSub = 16384; // ragged QB = 1 without the quarter / half first rows (exact)
+// Feature bit (product, not an ablation): uniform QB = 1 DYN launches of
+// 4096-byte RAW items also store each whole round's crc0 -- the 32 items as one
+// 128 KiB run -- at a.round_out[round] (rpc_crc32_device_large's contiguous
+// path folds those instead of the per-chunk CRCs).  The lane tree's maps
+// A_{8 KiB .. 64 KiB} sit in the image's ZI slots z = 12..15 (kLdsRoundMaps),
+// which such launches never read (16-byte aligned items of 4096 bytes have no
+// trailing pad; the host requires the aligned base).
+constexpr int kRowsRoundOut = 32768;
 // QB = 1 software pipeline over rows (chain of row r+1 beside the merge of row r).
 #ifndef RPCCRC_ROWS_PIPE
 #define RPCCRC_ROWS_PIPE 1
@@ -568,6 +576,21 @@ __device__ __forceinline__ uint32_t rw_map(const uint8_t *lds, uint32_t s) {
   for (uint32_t k = 0; k < 4; ++k) {
     t[2 * k] = lds_ld(lds, __builtin_amdgcn_perm(xl4, kLdsRW2, 0x0C020104u + k) + k * 128u);
     t[2 * k + 1] = lds_ld(lds, __builtin_amdgcn_perm(xh4, kLdsRW2, 0x0C020104u + k) + k * 128u + 64u);
+  }
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// Per-lane A_{4096 * 2^l} (kRowsRoundOut's tree): l = 0 is rw_map; l = 1..4
+// read the [n][nib] maps at kLdsRoundMaps + (l - 1) * 512 (same addressing).
+template <uint32_t TAB>
+__device__ __forceinline__ uint32_t nib_map_at(const uint8_t *lds, uint32_t s) {
+  static_assert((TAB & 255u) == 0 && TAB < (1u << 24), "256-B aligned for the perm-formed address");
+  const uint32_t xl4 = (s << 2) & 0x3C3C3C3Cu, xh4 = (s >> 2) & 0x3C3C3C3Cu;
+  uint32_t t[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    t[2 * k] = lds_ld(lds, __builtin_amdgcn_perm(xl4, TAB, 0x0C020104u + k) + k * 128u);
+    t[2 * k + 1] = lds_ld(lds, __builtin_amdgcn_perm(xh4, TAB, 0x0C020104u + k) + k * 128u + 64u);
   }
   return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
@@ -1105,6 +1128,25 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         if (lane == 0) {
           *done = 0;
           __hip_atomic_store(&gen[slot], rnd + kDynSlots, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr ((ABL & kRowsRoundOut) != 0 && QB == 1 && !RAGGED) {
+          // the round's crc0: a 5-level lane tree (lanes 32..63 repeat 0..31);
+          // at level l the earlier 2^l-item run is shifted past the later one
+          if (cnt == kRound) {
+            uint32_t x = v;
+#pragma unroll
+            for (uint32_t l = 0; l < 5; ++l) {
+              uint32_t sh;
+              if (l == 0) sh = rw_map(lds, x);
+              else if (l == 1) sh = nib_map_at<kLdsRoundMaps>(lds, x);
+              else if (l == 2) sh = nib_map_at<kLdsRoundMaps + 512u>(lds, x);
+              else if (l == 3) sh = nib_map_at<kLdsRoundMaps + 1024u>(lds, x);
+              else sh = nib_map_at<kLdsRoundMaps + 1536u>(lds, x);
+              const uint32_t mine = ((lane >> l) & 1u) ? x : sh;
+              x = mine ^ (uint32_t)__shfl_xor((int)mine, 1 << l, 64);
+            }
+            if (lane == 0) a.round_out[base / kRound] = x;
+          }
         }
         j0 += cnt;
       }

@@ -320,6 +320,7 @@ struct DeviceCtx {
   int device = -1;
   int cus = 0;
   uint4 *img = nullptr; // LDS table image (rows kernel layout, 155 KiB)
+  uint4 *img_round = nullptr; // the same with the round maps in ZI[11..14] (crc32_layout.h kLdsRoundMaps)
   uint32_t *tq = nullptr;
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
   uint32_t *big_dbl = nullptr; // the big-body fold's doubling maps per chunk class (build_big_dbl)
@@ -407,6 +408,12 @@ const bool g_big_span = [] {
   return !(e && e[0] == '0');
 }();
 constexpr uint64_t kSpanMinBytes = 1ull << 20;
+// Round values for one-row chunks of contiguous large bodies (device_large):
+// on by default; RPCCRC_ROUND_COMBINE=0 folds the per-chunk CRCs.
+const bool g_round_combine = [] {
+  const char *e = getenv("RPCCRC_ROUND_COMBINE");
+  return !(e && e[0] == '0');
+}();
 constexpr bool kAutoSplitFrames = true;           // AUTO frames batches: split (true) or packed (false)
 constexpr uint64_t kPackedMaxSlices = 1ull << 21; // slice-table cap (8 MiB)
 // Chunks per packed slice, at least: a slice switch costs the wave two scalar
@@ -451,6 +458,7 @@ void init_device(int dev) {
   (void)hipSetDevice(dev);
   hipError_t e = hipSuccess;
   e = (e == hipSuccess) ? hipMalloc(&c.img, kImgHbmBytes) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.img_round, kImgHbmBytes) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.big_dbl, kBigDblWords * 4) : e;
@@ -459,13 +467,18 @@ void init_device(int dev) {
   if (e == hipSuccess) *reinterpret_cast<volatile uint32_t *>(c.err) = 0;
   if (e == hipSuccess) {
     build_lds_image_v2(img.data());
-    if (kImgCompact) {
+    std::vector<uint32_t> img_round(img);
+    for (uint32_t l = 1; l <= 4; ++l) // A_{4096 * 2^l} = NIB[12 + l]
+      std::copy(nib.begin() + (12 + l) * 128, nib.begin() + (13 + l) * 128,
+                img_round.begin() + kLdsRoundMaps / 4 + (l - 1) * 128);
+    auto upload = [&](uint4 *dst, const std::vector<uint32_t> &src) {
+      if (!kImgCompact) return hipMemcpy(dst, src.data(), kLdsBytesV3, hipMemcpyHostToDevice);
       std::vector<uint32_t> compact(kImgCompactBytes / 4);
-      build_lds_image_compact(img.data(), compact.data());
-      e = hipMemcpy(c.img, compact.data(), kImgCompactBytes, hipMemcpyHostToDevice);
-    } else {
-      e = hipMemcpy(c.img, img.data(), kLdsBytesV3, hipMemcpyHostToDevice);
-    }
+      build_lds_image_compact(src.data(), compact.data());
+      return hipMemcpy(dst, compact.data(), kImgCompactBytes, hipMemcpyHostToDevice);
+    };
+    e = upload(c.img, img);
+    if (e == hipSuccess) e = upload(c.img_round, img_round);
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);
@@ -883,7 +896,16 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   const uint64_t cs = max_nch / 4096;
   const bool contig = fast && min_nch == max_nch && max_nch % 4096 == 0 && cs >= 1 && cs <= 16 &&
                       (chunk & (chunk - 1)) == 0 && n <= 1024;
-  const size_t ws_bytes = fast ? total * 4 + 64 : n * sizeof(BodyDesc) + n * 16 + total * (8 + 4 + 4) + 64;
+  // One-row chunks of a contiguous batch: the rows pass also stores each round's
+  // crc0 (32 chunks = 128 KiB, ItemsArgs.round_out) and the combine folds those
+  // -- 1/32 of the values (RPCCRC_ROUND_COMBINE=0: the per-chunk fold).  The
+  // launch must deal in DYN rounds (launch_rows: >= 8 rounds per workgroup),
+  // and the base must be 16-byte aligned: the round maps sit in the image's ZI
+  // slots of trailing pads 12..15, which a misaligned base's items would read.
+  const bool rounds = contig && chunk == 4096 && g_round_combine && total >= 8ull * 32 * (uint64_t)max_blocks_for(c) &&
+                      (reinterpret_cast<uintptr_t>(d_base + h_offsets[0]) & 15u) == 0;
+  const size_t ws_bytes = fast ? total * 4 + (rounds ? total / 8 : 0) + 64
+                               : n * sizeof(BodyDesc) + n * 16 + total * (8 + 4 + 4) + 64;
   Lease wsl;
   if (const int rc = wsl.get(c.ws, ws_bytes, s)) return rc;
   uint8_t *ws = wsl.ptr();
@@ -900,6 +922,10 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
     if (contig) {
       k.zero_out = d_out;
       k.zero_n = (uint32_t)n;
+    }
+    if (rounds) {
+      k.round_out = d_raw + total;
+      k.lds_image = c.img_round;
     }
     RPCCRC_TRY(launch_rows(k, 1, nontemporal(), max_blocks_for(c), s, sl.done_event(), &sl.recorded));
   } else {
@@ -935,6 +961,11 @@ int device_large(const DeviceCtx &c, const uint8_t *d_base, const uint64_t *h_of
   if (contig) {
     ca.contig = true;
     ca.splits = (uint32_t)cs;
+  }
+  if (rounds) { // 128 * S round values per body: one block each
+    ca.raw = d_raw + total;
+    ca.chunk = chunk * 32;
+    ca.splits = 1;
   }
   ca.inline_bodies = inl;
   if (inl) ca.bodies = ib;

@@ -475,6 +475,31 @@ def test_device_large_equal_bodies_combine(chunk, blen, nb, gap):
     assert got.tolist() == [oracle.crc32(host[o:o + blen]) for o in offs]
 
 
+@pytest.mark.parametrize("blen,nb,misalign", [
+    (16 << 20, 16, 0),   # 64Ki one-row chunks: the smallest batch with round values on 256 CUs
+    (48 << 20, 6, 16),   # S = 3 (384 round values per body)
+    (256 << 20, 1, 0),   # one C4 body (S = 16: 2048 round values)
+    (256 << 20, 1, 3),   # misaligned base (trailing pads 13): per-chunk fold
+    (48 << 20, 6, 5),    # misaligned base (pads 11): per-chunk fold
+    (16 << 20, 8, 0),    # 32Ki chunks: too few rounds per workgroup, per-chunk fold
+])
+def test_device_large_round_values(blen, nb, misalign):
+    """Back-to-back equal bodies of a multiple of 16 MiB (4 KiB chunks): the rows
+    pass also stores each 32-chunk round's crc0 (ItemsArgs.round_out, a lane tree
+    over the image's round maps) and the contiguous combine folds those.  Bases
+    that are not 16-byte aligned keep the per-chunk fold (the round maps share
+    the image slots of trailing pads 12..15)."""
+    base = torch.empty((misalign + nb * blen + 16 + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, 0x20D0 + nb)
+    offs = [misalign + i * blen for i in range(nb)]
+    got = u32(rpc_amd.device_large(base, offs, [blen] * nb))
+    torch.cuda.synchronize()
+    assert rpc_amd.device_status() == 0
+    want = oracle.crc32_batch_mt(base.cpu().numpy(), np.array(offs, dtype=np.uint64),
+                                 np.full(nb, blen, dtype=np.uint64))
+    assert got.tolist() == want.tolist()
+
+
 def test_tail_stealing_back_to_back_launches():
     """Uniform one-row batches deal their last rounds from a leased device counter
     that each launch's last workgroup resets (crc32_rows.h kStealAhead).  70
