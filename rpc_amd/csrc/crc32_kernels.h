@@ -111,6 +111,13 @@ struct BigRoute {
   uint32_t *blk = nullptr;
   uint64_t span_rows_max = 0;
   const uint4 *tab4 = nullptr; // span mode: the slice-by-4 tables (scalar table image, first 4 KiB)
+  // Span mode with round values (ItemsArgs.round_out): the span pass also stores
+  // the crc0 of every whole 32-block round (128 KiB) at rnd[round], and the fold
+  // takes a body's whole rounds from there.  rnd_image: the table image with the
+  // round maps (kLdsRoundMaps).  Set by the host only when the span pass deals in
+  // DYN rounds (span_rows_max >= 256 * max_blocks).
+  uint32_t *rnd = nullptr;
+  const uint4 *rnd_image = nullptr;
   // Frames verify in route-all mode: the fold also decides each frame's verdict
   // (frames_compare_kernel's rule: the parse's pre-verdict, else crc == the
   // header's crc32), so the compare launch is skipped.  nullptr: no verdicts.

@@ -288,7 +288,7 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   }
   if (k.steal_s == 0) k.steal = nullptr;
   if (a.round_out != nullptr) { // kRowsRoundOut: whole DYN rounds of 4096-byte uniform RAW items
-    if (QB != 1 || ragged || !dyn || a.len != 4096 || a.stride != 4096 || a.mode != kModeRaw || a.n_dev != nullptr ||
+    if (QB != 1 || ragged || !dyn || a.len != 4096 || a.stride != 4096 || a.mode != kModeRaw ||
         a.out_idx != nullptr || (reinterpret_cast<uintptr_t>(a.base) & 15u) != 0)
       return hipErrorInvalidValue;
 #define RPCCRC_ROWS_ROUND(N)                                                                                      \
@@ -1034,20 +1034,45 @@ __global__ void __launch_bounds__(kFoldThreads) big_combine_aligned_kernel(const
     const uint64_t m = nch ? nch - 1 : 0; // chunks folded into G: the head, then blocks j0 + 1 ..
     uint32_t acc = 0;
     constexpr uint32_t kB = kFoldBatch;
-    for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * kFoldThreads) {
-      uint32_t rv[kB];
+    // G' = crc0 of the interior blocks [ja, jb) (jb = j1), shifted to jb.  With
+    // round values: the whole rounds [ra, rb) from rnd[], the <= 31 blocks before
+    // them (wave 2) and after them (wave 3) from blk[], each shifted to jb.
+    const uint64_t ja = j0 + 1, jb = j1, ra = (ja + 31) >> 5, rb = jb >> 5;
+    if (r.rnd != nullptr && m > 1 && ra < rb) {
+      const uint64_t nA = (ra << 5) - ja, nR = rb - ra, nC = jb - (rb << 5);
+      const uint32_t *rstep = nib + 128u * (17u + kFoldLog2); // A_{T * 128 KiB}
+      for (uint64_t k0 = t; k0 < nR; k0 += (uint64_t)kB * kFoldThreads) {
+        uint32_t rv[kB];
 #pragma unroll
-      for (uint32_t q = 0; q < kB; ++q) {
-        const uint64_t k = k0 + q * kFoldThreads;
-        rv[q] = (k != 0 && k < m) ? r.blk[j0 + k] : 0u;
+        for (uint32_t q = 0; q < kB; ++q) {
+          const uint64_t k = k0 + q * kFoldThreads;
+          rv[q] = (k < nR) ? r.rnd[ra + k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kB; ++q)
+          if (k0 + q * kFoldThreads < nR) acc = nib_map(rstep, acc) ^ rv[q];
       }
+      if (t < nR) // from this thread's last round to the end of the rounds, then past C
+        acc = apply((((nR - 1 - t) % kFoldThreads) << 17) + (nC << 12), acc);
+      const uint32_t u = t & 63u;
+      if (w == 2u && u < nA) acc ^= apply((jb - 1 - (ja + u)) << 12, r.blk[ja + u]);
+      if (w == 3u && u < nC) acc ^= apply((nC - 1 - u) << 12, r.blk[(rb << 5) + u]);
+    } else {
+      for (uint64_t k0 = t; k0 < m; k0 += (uint64_t)kB * kFoldThreads) {
+        uint32_t rv[kB];
 #pragma unroll
-      for (uint32_t q = 0; q < kB; ++q)
-        if (k0 + q * kFoldThreads < m) acc = nib_map(stepnib, acc) ^ rv[q];
-    }
-    if (t < m) {
-      for (uint32_t j = (uint32_t)((m - 1 - t) % kFoldThreads); j; j &= j - 1)
-        acc = nib_map(nib + 128u * (lc + (uint32_t)__builtin_ctz(j)), acc);
+        for (uint32_t q = 0; q < kB; ++q) {
+          const uint64_t k = k0 + q * kFoldThreads;
+          rv[q] = (k != 0 && k < m) ? r.blk[j0 + k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kB; ++q)
+          if (k0 + q * kFoldThreads < m) acc = nib_map(stepnib, acc) ^ rv[q];
+      }
+      if (t < m) {
+        for (uint32_t j = (uint32_t)((m - 1 - t) % kFoldThreads); j; j &= j - 1)
+          acc = nib_map(nib + 128u * (lc + (uint32_t)__builtin_ctz(j)), acc);
+      }
     }
     for (int d = 1; d < 64; d <<= 1) acc ^= (uint32_t)__shfl_xor((int)acc, d, 64);
     if (lane == 0) part[w] = acc;
@@ -1121,7 +1146,7 @@ __global__ void __launch_bounds__(kFoldThreads) big_combine_aligned_kernel(const
 size_t big_route_workspace_bytes(uint64_t n, uint64_t span_rows) {
   return align256((n + 63) / 64 * 8) + align256(64) + align256(kBigMaxBodies * 4) +
          align256((kBigMaxBodies + 1) * 8) + align256(kBigMaxChunks * 8) + 2 * align256(kBigMaxChunks * 4) +
-         (span_rows ? align256((span_rows + 1) * 4) : 0);
+         (span_rows ? align256((span_rows + 1) * 4) + align256((span_rows / 32 + 1) * 4) : 0);
 }
 
 BigRoute big_route_carve(void *ws, uint64_t n, uint64_t span_rows) {
@@ -1141,6 +1166,7 @@ BigRoute big_route_carve(void *ws, uint64_t n, uint64_t span_rows) {
   r.c_raw = reinterpret_cast<uint32_t *>(take(kBigMaxChunks * 4));
   if (span_rows) {
     r.blk = reinterpret_cast<uint32_t *>(take((span_rows + 1) * 4)); // (+1: the fold's idle loads read blk[j0])
+    r.rnd = reinterpret_cast<uint32_t *>(take((span_rows / 32 + 1) * 4)); // (the host clears it when unused)
     r.span_rows_max = span_rows;
   }
   return r;
@@ -1219,6 +1245,11 @@ hipError_t launch_big_route(const ItemsArgs &proto, const BigRoute &r, const uin
     u.big_min = 0xFFFFFFFFu;
     u.mode = kModeRaw;
     u.out = r.blk;
+    if (r.rnd != nullptr) { // round values (crc32_rows.h kRowsRoundOut)
+      if (!r.rnd_image || r.span_rows_max < 256ull * (uint64_t)max_blocks) return hipErrorInvalidValue;
+      u.round_out = r.rnd;
+      u.lds_image = r.rnd_image;
+    }
     u.steal = span.p;
     e = launch_rows(u, 1, nt, max_blocks, s, span.done, span.recorded);
     if (e != hipSuccess) return e;

@@ -728,6 +728,9 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     r.tq = c.tq;
     r.dbl = c.big_dbl;
     r.tab4 = c.scalar_tab;
+    // span pass round values: only when it deals in DYN rounds
+    if (!(span_rows && g_round_combine && span_rows >= 256ull * (uint64_t)mb)) r.rnd = nullptr;
+    r.rnd_image = c.img_round;
     if (route_all) {
       r.all_n = (uint32_t)n;
       if (cmp) {

@@ -217,7 +217,9 @@ def test_aligned_fold_matches_zlib(L, start, chunk, nt):
 # chunk pass CRCs each body's first and last partial blocks (pieces 2b, 2b + 1).
 
 
-def span_fold_emulated(mem: bytes, s: int, L: int, nt: int) -> int:
+def span_fold_emulated(mem: bytes, s: int, L: int, nt: int, rs: int = 0) -> int:
+    """big_combine_aligned_kernel's span branch; rs > 0: with round values of rs
+    blocks (the product's 32), whole rounds from the round table."""
     if L == 0:
         return 0
     e = s + L
@@ -232,6 +234,28 @@ def span_fold_emulated(mem: bytes, s: int, L: int, nt: int) -> int:
     m = nch - 1
     raw = [0] + [crc0(mem[(j0 + k) << 12:(j0 + k + 1) << 12]) for k in range(1, m)]  # G' leaves chunk 0 out
     g = 0
+    ja, jb = j0 + 1, j1
+    ra, rb = (ja + rs - 1) // rs if rs else 0, jb // rs if rs else 0
+    if rs and m > 1 and ra < rb:
+        # whole rounds (their crc0 as the span pass stores it), thread-strided Horner
+        # with A_{nt * rs * 4096}, then the <= rs - 1 blocks before / after them
+        blk = lambda j: crc0(mem[j << 12:(j + 1) << 12])  # noqa: E731
+        rv = [crc0(mem[(r * rs) << 12:((r + 1) * rs) << 12]) for r in range(ra, rb)]
+        nA, nR, nC = ra * rs - ja, rb - ra, jb - rb * rs
+        for t in range(nt):
+            acc, kk = 0, t
+            while kk < nR:
+                acc = nib_shift(nt * rs * 4096, acc) ^ rv[kk]
+                kk += nt
+            if t < nR:
+                acc = nib_shift(((nR - 1 - t) % nt) * rs * 4096 + nC * 4096, acc)
+            g ^= acc
+        for u in range(nA):
+            g ^= nib_shift((jb - 1 - (ja + u)) * 4096, blk(ja + u))
+        for u in range(nC):
+            g ^= nib_shift((nC - 1 - u) * 4096, blk(rb * rs + u))
+        g ^= nib_shift((m - 1) * 4096, head ^ seed)
+        return ~(nib_shift(e - (j1 << 12), g) ^ tail) & 0xFFFFFFFF
     for t in range(nt):
         acc, kk = 0, t
         while kk < m:
@@ -254,3 +278,19 @@ def test_span_fold_matches_zlib(L, start, nt):
     rnd = random.Random(L * 13 + start)
     mem = bytearray(rnd.randbytes(start + L + 4096))
     assert span_fold_emulated(bytes(mem), start, L, nt) == zlib.crc32(bytes(mem[start:start + L]))
+
+
+@pytest.mark.parametrize("L,start,nt,rs", [
+    (4096 * 9, 5, 2, 4),            # rounds of 4 blocks: one whole round inside, blocks around it
+    (4096 * 8, 0, 2, 4),            # body starting on a round boundary (its head is a whole block)
+    (4096 * 12 - 1, 4096 * 4, 3, 4),
+    (4096 * 40 + 77, 123, 4, 4),    # several rounds per thread
+    (4096 * 7, 4096 * 3 + 1, 2, 4), # interior shorter than a round: per-block fold
+    (4096 * 70 + 3, 4096 * 31, 2, 32),  # the product's 32-block rounds: one whole round
+])
+def test_span_fold_round_values_matches_zlib(L, start, nt, rs):
+    """Span mode with round values (BigRoute.rnd): whole rounds from the round
+    table, the blocks before and after them from the block table."""
+    rnd = random.Random(L * 7 + start)
+    mem = bytearray(rnd.randbytes(start + L + 4096))
+    assert span_fold_emulated(bytes(mem), start, L, nt, rs) == zlib.crc32(bytes(mem[start:start + L]))

@@ -320,6 +320,79 @@ def test_frames_lifted_cap_span_mode(sparse):
     assert all(v[i] == rpc_amd.FRAME_BAD_CRC for i in flips)
 
 
+def test_frames_lifted_cap_span_mode_round_values():
+    """Span mode over a stream of >= 256 MiB: the span pass deals in DYN rounds and
+    also stores each 32-block round's crc0 (BigRoute.rnd), which the fold takes for
+    a body's whole rounds; the blocks before and after them come from the block
+    table.  Bodies starting and ending on round boundaries (128 KiB), whole rounds
+    with no blocks around them, random lengths up to 3 MiB and a 64 MiB body; stamp
+    then verify, then flipped bytes inside a whole round, in the blocks before the
+    first round and after the last one."""
+    R = 128 << 10
+    rng = np.random.default_rng(0x20D5)
+    lens, pos = [], 0
+
+    def add(L):
+        nonlocal pos
+        lens.append(L)
+        pos += HDR + L
+
+    def align_next_body():  # a filler frame so that the next body starts on a round boundary
+        add((-(pos + 2 * HDR)) % R)
+
+    add((64 << 20) + 3 * 4096 + 5)  # blocks 1..31 before its first whole round, 3 after its last
+    for k in range(60):
+        add(int(rng.integers(0, 3 << 20)))
+        if k % 6 == 0:
+            align_next_body()
+            add([R, 3 * R, 2 * R + 4096, 5 * R - 1, R + 1][k // 6 % 5])
+    align_next_body()
+    add(40 * R)  # whole rounds only
+    while pos < (260 << 20):
+        add(int(rng.integers(1 << 20, 4 << 20)))
+    total = pos
+    offs = np.cumsum([0] + [HDR + L for L in lens[:-1]]).astype(np.uint64)
+    base = aligned_stream(total)
+    fill = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(fill, 0x20D6)
+    base.copy_(fill[:total])
+    del fill
+    do = to_dev(offs.view(np.int64))
+    dl = to_dev(np.array(lens, dtype=np.uint32).view(np.int32))
+    sv = rpc_amd.frames_stamp(base, do, dl, lift_cap=True, stream_bytes=total)
+    assert sv.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(lens)
+    host = base.cpu().numpy()
+    want = oracle.crc32_batch_mt(host, offs + np.uint64(HDR), np.array(lens, dtype=np.uint64))
+    hdr_crc = [int.from_bytes(host[int(o) + 8:int(o) + 12].tobytes(), "big") for o in offs]
+    assert hdr_crc == want.tolist()
+    v, c = rpc_amd.frames_verify(base, do, lift_cap=True, stream_bytes=total)
+    assert v.cpu().numpy().tolist() == [rpc_amd.FRAME_OK] * len(lens)
+    assert u32(c).tolist() == want.tolist()
+    # flips: a whole round in the middle of the 64 MiB body, its first interior
+    # block (before its first whole round), its last interior block (after the last)
+    assert (int(offs[0]) + HDR + lens[0]) // 4096 % 32 == 3
+    b0 = int(offs[0]) + HDR
+    e0 = b0 + lens[0]
+    k_last = len(lens) - 1
+    flips = {0: [b0 + (20 << 20) + 77], k_last: [int(offs[k_last]) + HDR + lens[k_last] // 2]}
+    first_inner = (b0 + 4095) // 4096 * 4096 + 10
+    last_inner = (e0 // 4096 - 1) * 4096 + 4000
+    flips[0] += [first_inner, last_inner]
+    for p in sum(flips.values(), []):
+        base[p] ^= 0x10
+    v, _ = rpc_amd.frames_verify(base, do, lift_cap=True, stream_bytes=total)
+    v = v.cpu().numpy().tolist()
+    assert [i for i, x in enumerate(v) if x != rpc_amd.FRAME_OK] == sorted(flips)
+    # each flip alone: one bad frame each time
+    for p in sum(flips.values(), []):
+        base[p] ^= 0x10
+    for p, i in [(first_inner, 0), (last_inner, 0)]:
+        base[p] ^= 0x01
+        v, _ = rpc_amd.frames_verify(base, do, lift_cap=True, stream_bytes=total)
+        assert [j for j, x in enumerate(v.cpu().numpy().tolist()) if x != rpc_amd.FRAME_OK] == [i]
+        base[p] ^= 0x01
+
+
 @pytest.mark.parametrize("role", ["server", "client"])
 def test_frames_lifted_cap_span_mode_verdicts(role):
     """Span mode (4 KiB-aligned dense stream of >= 1 MiB) with every verdict the

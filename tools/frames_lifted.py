@@ -20,4 +20,5 @@ for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
     r["big_aligned"] = os.environ.get("RPCCRC_BIG_ALIGNED", "default")
     r["big_chunk"] = os.environ.get("RPCCRC_BIG_CHUNK", "default")
     r["big_span"] = os.environ.get("RPCCRC_BIG_SPAN", "default")
+    r["round_combine"] = os.environ.get("RPCCRC_ROUND_COMBINE", "default")
     print(json.dumps(r), flush=True)

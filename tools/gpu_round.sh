@@ -68,6 +68,13 @@ for s in $STEPS; do
                RPCCRC_BIG_SPAN=$v run frames_span${v}_$i 300 python tools/frames_lifted.py 2 || exit 1
              done
            done ;;
+    frames_round_ab) # interleaved, order rotated: span-pass round values on (1) / off (0)
+           for i in 1 2 3; do
+             if [ $((i % 2)) = 1 ]; then order="1 0"; else order="0 1"; fi
+             for v in $order; do
+               RPCCRC_ROUND_COMBINE=$v run frames_round${v}_$i 300 python tools/frames_lifted.py 2 || exit 1
+             done
+           done ;;
     frames_libs) # lifted-cap frames probe per library (A/B): FRAMES_LIBS="head name ..."
            for i in 1 2; do
              for l in ${FRAMES_LIBS:-head}; do
