@@ -803,13 +803,13 @@ __global__ void __launch_bounds__(1024) big_plan_aligned_kernel(const uint8_t *b
     for (uint64_t b = t; b < nb; b += 1024) {
       uint64_t s0, L;
       if (r.parse.frame_off != nullptr) {
-        frames_parse_one(r.parse, b);
-        s0 = r.parse.body_off[b]; // (this thread's own store)
-        L = r.parse.body_len[b];
+        const FrameBody fb = frames_parse_one(r.parse, b);
+        s0 = fb.off;
+        L = fb.len;
       } else if (r.stamp.frame_off != nullptr) {
-        frames_stamp_prep_one(r.stamp, b);
-        s0 = r.stamp.body_off[b];
-        L = r.stamp.len_eff[b];
+        const FrameBody fb = frames_stamp_prep_one(r.stamp, b);
+        s0 = fb.off;
+        L = fb.len;
         // Span mode's fold reads the partial blocks while it writes headers:
         // only frames in stream order, none overlapping the next, keep every
         // header out of every body (else the chunk route: all CRCs first).

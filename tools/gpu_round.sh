@@ -75,9 +75,11 @@ for s in $STEPS; do
                RPCCRC_ROUND_COMBINE=$v run frames_round${v}_$i 300 python tools/frames_lifted.py 2 || exit 1
              done
            done ;;
-    frames_libs) # lifted-cap frames probe per library (A/B): FRAMES_LIBS="head name ..."
-           for i in 1 2; do
-             for l in ${FRAMES_LIBS:-head}; do
+    frames_libs) # lifted-cap frames probe per library (A/B, order rotated): FRAMES_LIBS="head name ..."
+           read -r -a FL <<< "${FRAMES_LIBS:-head}"
+           for i in 1 2 3; do
+             for j in $(seq 0 $((${#FL[@]} - 1))); do
+               l=${FL[$(( (j + i - 1) % ${#FL[@]} ))]}
                if [ "$l" = head ]; then lib=""; else lib=$PWD/abtest/$l.so; fi
                RPCCRC_LIB=$lib run frames_${l}_$i 300 python tools/frames_lifted.py 2 || exit 1
              done
