@@ -64,8 +64,8 @@ def test_drop_in_golden_random(golden):
 def test_drop_in_large_bodies():
     # device copy and chunked paths; exact multiples of 16 MiB take the one-row-chunk
     # contiguous combine, whose atomics now target a device word, not
-    # the pinned host result
-    for n in [(8 << 20) - 1, (8 << 20) + 13, (17 << 20) + 5, 16 << 20, 32 << 20, 48 << 20]:
+    # the pinned host result; 256 MiB: 64Ki one-row chunks, the rows pass's round values
+    for n in [(8 << 20) - 1, (8 << 20) + 13, (17 << 20) + 5, 16 << 20, 32 << 20, 48 << 20, 256 << 20]:
         data = oracle.splitmix_bytes(n, n)
         assert rpc_amd.rpc_crc32(data) == oracle.crc32(data), n
 
