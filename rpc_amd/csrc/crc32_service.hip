@@ -107,6 +107,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     uint32_t instance) {
   __shared__ uint32_t s_last;  // low 32 bits of the last request's s_memrealtime
   __shared__ uint32_t s_alive; // waves still in the loop
+  // Tq of the inline lengths: an LDS read instead of a dependent global load per
+  // request (476 B of LDS still fits beside any rows workgroup: <= 163040 B)
+  __shared__ uint32_t s_tq[kSvcInline + 1];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -114,6 +117,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     s_last = (uint32_t)t_start;
     s_alive = kSvcWaves;
   }
+  for (uint32_t k = threadIdx.x; k <= kSvcInline; k += 64 * kSvcWaves) s_tq[k] = tq[k];
   __syncthreads();
   static_assert(kSvcPer == 2, "one poll: 2 request blocks x 32 dwords");
   // per-lane constants: shift of this lane's segment to V's end, per seg class
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
         if (!pend[i]) continue;
         const uint32_t len = lens[i], seg = svc::seg_of(len);
         const uint32_t c0 = body_crc0(body[i], seg, len, lane, seg == 4u ? k4 : seg == 8u ? k8 : k16);
-        const uint32_t crc = len == 0u ? 0u : ~(tq[len] ^ c0);
+        const uint32_t crc = len == 0u ? 0u : ~((inl[i] ? s_tq[len] : tq[len]) ^ c0);
         if (lane == 0)
           __hip_atomic_store(&sh->res[wave + kSvcWaves * i][0], (uint64_t)crc | ((uint64_t)seqs[i] << 32),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -15,6 +15,8 @@ import rpc_amd  # noqa: E402
 
 DEV = "cuda:0"
 n, L = 1 << 18, 4096
+if os.environ.get("SVC_BATCH_LEN") == "1024":  # the QB = 4 rows kernel (the largest LDS): 1M x 1 KiB
+    n, L = 1 << 20, 1024
 if os.environ.get("SVC_MAXBLOCKS"):  # persistent-grid cap (a placement test)
     rpc_amd.set_options(True, int(os.environ["SVC_MAXBLOCKS"]))
 x = torch.empty(n * L, dtype=torch.uint8, device=DEV)
