@@ -622,15 +622,23 @@ struct QuarterInfo {
 // whole 128-B line.
 // kDynRound / dyn_round(QB): crc32_kernels.h (the host sizes launches with them).
 // Rounds the LDS output ring holds: a wave that finishes a task of round r
-// waits until round r - kDynSlots has been stored.  8 (was 4): C2 -1.0 %, NS
-// -0.25 % (profiles/r02/r02bx_dyn_slots_ab.txt); the QB = 4 ring then takes
-// 4 KiB, which still fits beside the 155 KiB image.
+// waits until round r - kDynSlots has been stored.  QB = 1: 8 (was 4): C2
+// -1.0 %, NS -0.25 % (profiles/r02/r02bx_dyn_slots_ab.txt).  QB = 4: 6 (its
+// ring is 512 B a slot): with 8 the kernel took 163040 B of LDS, and a CU
+// running one of its workgroups had no room left for the drop-in service's
+// (kRowsLdsMax below) -- a C1 batch beside a busy service ran 251 us against
+// 161 with 6 slots, while C1 alone measured the same (157.1 / 157.3 us,
+// profiles/r04za).
 #ifndef RPCCRC_DYN_SLOTS
-#define RPCCRC_DYN_SLOTS 8
+#define RPCCRC_DYN_SLOTS 6
 #endif
 #ifndef RPCCRC_DYN_SLOTS_QB1
-#define RPCCRC_DYN_SLOTS_QB1 RPCCRC_DYN_SLOTS
+#define RPCCRC_DYN_SLOTS_QB1 8
 #endif
+// LDS one rows workgroup may take: the rest of the CU's 160 KiB stays free for
+// the drop-in service's workgroup (crc32_service.hip, 476 B; LDS is granted in
+// 1 KiB steps as measured: 162016 B left room for it, 163040 B did not).
+constexpr uint32_t kRowsLdsMax = 163840u - 1024u;
 constexpr uint32_t dyn_slots(int QB) { return QB == 1 ? RPCCRC_DYN_SLOTS_QB1 : RPCCRC_DYN_SLOTS; }
 // Tail stealing (DYN with a.steal_s > 0): workgroup vb keeps only its first
 // steal_s local rounds static (global rounds r * blocks + vb); the remaining
@@ -725,6 +733,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // DYN control block (dyn_ring_words): task counter, done counts, slot
   // generations (slot s starts at round s), CRC ring.
   __shared__ uint32_t s_ctl[DYN ? (STEAL ? dyn_ctl_words(QB) : dyn_ring_words(QB)) : 1];
+  static_assert(sizeof(s_lds) + sizeof(s_ctl) <= kRowsLdsMax, "leave a CU room for the drop-in service");
   // kEarlyRow: each wave's first task is static (DYN: counter index = wave, so
   // the LDS counter starts at 16), and its first row's loads are issued between
   // the image's global loads and its LDS stores -- the row's HBM latency then
