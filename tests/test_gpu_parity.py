@@ -888,17 +888,19 @@ def test_c3_per_rank_shard_full_coverage():
         del part
 
 
-def test_drop_in_service_beside_batches():
-    """The drop-in service (crc32_service.hip, one resident workgroup with no LDS
-    table) must share the chip with the rows kernel's persistent grid (one
-    155 KiB-LDS workgroup per CU): north-star-sized batches while another thread
-    keeps the service busy run at about their normal time (a workgroup that could
-    not be placed would double it), and every CRC of both is exact."""
+@pytest.mark.parametrize("n,L", [(1 << 18, 4096), (1 << 20, 1024)])
+def test_drop_in_service_beside_batches(n, L):
+    """The drop-in service (crc32_service.hip, one resident workgroup with 476 B
+    of LDS) must share the chip with the rows kernel's persistent grid (one
+    155-159 KiB-LDS workgroup per CU): batches while another thread keeps the
+    service busy run at about their normal time (a workgroup that could not be
+    placed would take ~1.5x), and every CRC of both is exact.  1M x 1 KiB is the
+    QB = 4 kernel, the largest LDS footprint (an 8-slot ring left no room:
+    251 vs 161 us, profiles/r04za)."""
     import time
-    n, L = 1 << 18, 4096
     x = torch.empty(n * L, dtype=torch.uint8, device=DEV)
     rpc_amd.fill_random(x, 0x5E7)
-    want = oracle.crc32_uniform(x.cpu().numpy(), n, L)
+    want = oracle.crc32_uniform_mt(x.cpu().numpy(), n, L)
     bodies = [oracle.splitmix_bytes(k, 0xD0 + k) for k in (12, 68, 300, 1000, 1024)]
     wants = [oracle.crc32(b) for b in bodies]
 
