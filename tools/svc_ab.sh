@@ -1,6 +1,10 @@
 #!/bin/bash
 # Drop-in service A/B (in-tree library vs abtest/scalar_bench_base linked to abtest/baselib),
 # rotated, then the service beside rows launches (NS-shaped and C1-shaped batches).
+# The base side is built in this container first:
+#   mkdir -p abtest/baselib && cp abtest/base.so abtest/baselib/librpccrc.so &&
+#   gcc -O2 -std=c11 -D_POSIX_C_SOURCE=200809L -Iinclude -o abtest/scalar_bench_base \
+#       tools/scalar_bench.c -Labtest/baselib -lrpccrc -Wl,-rpath,'$ORIGIN/baselib' -ldl -lpthread
 mkdir -p gpurun_out/r04z
 for r in 1 2 3; do
   if [ $((r % 2)) = 1 ]; then order="head base"; else order="base head"; fi
