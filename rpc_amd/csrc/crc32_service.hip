@@ -30,10 +30,11 @@
 // that arrives while an instance is leaving is picked up by the next one:
 // pending = seq not yet answered in res).
 //
-// Resources: NO table image in LDS and few registers (37 VGPRs; built without
-// the library's max-ilp scheduler, Makefile), so the kernel can sit
-// on a CU next to a rows-kernel workgroup (155 KiB LDS each, one per CU, a
-// persistent grid over all CUs): the CRC is bit-serial --
+// Resources: no table image in LDS (476 B: the Tq words of the inline
+// lengths) and few registers (37 VGPRs; built without the library's max-ilp
+// scheduler, Makefile), so the kernel can sit on a CU next to a rows-kernel
+// workgroup (155-159 KiB LDS each, one per CU, a persistent grid over all CUs;
+// crc32_rows.h kRowsLdsMax keeps 1 KiB free for it): the CRC is bit-serial --
 //   chain: crc0 of each 32-bit word by the bit loop (3 VALU per bit);
 //   merge: lane L's segment crc0 times x^(8 * seg * (63 - L)) mod P (per-lane
 //          constant from the host, kSvcShift), bit-serial, then an XOR over
