@@ -235,6 +235,22 @@ static double steal_frac(int QB = 1) {
   static const double f4 = env_frac("RPCCRC_STEAL_FRAC_QB4", f1);
   return QB == 4 ? f4 : f1;
 }
+// ... but at most this many pool rounds per workgroup: the pool has to absorb
+// the workgroups' spread in finishing time, not a share of an ever larger
+// batch, and every pool round costs a device-scope claim.  C3 (8M x 4 KiB,
+// 1024 rounds per workgroup): 15 % 4778 us, 5 % 4724 us, 30 % 4846 us
+// (profiles/r04zf, rotated); with this cap of 48 (4.7 %) 4752 against 4789 us
+// uncapped (r04zg); caps of 16 / 24 / 32 were within that box's noise (r04zh).
+// The north star (128 rounds per workgroup, 19 in the pool) and smaller
+// launches are below the cap.  RPCCRC_STEAL_MAX_PER_WG overrides it (A/B).
+static uint32_t steal_max_per_wg() {
+  static const uint32_t v = [] {
+    const char *e = getenv("RPCCRC_STEAL_MAX_PER_WG");
+    const long x = e ? atol(e) : 0;
+    return x > 0 ? (uint32_t)x : 48u;
+  }();
+  return v;
+}
 
 hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipStream_t stream, hipEvent_t steal_done,
                        bool *steal_recorded) {
@@ -279,9 +295,11 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   ItemsArgs k = a;
   k.steal_s = 0;
   k.steal_permille = (uint32_t)(steal_frac(QB) * 1000.0 + 0.5);
+  k.steal_max_wg = steal_max_per_wg();
   if (dyn && a.steal != nullptr && a.n_dev == nullptr) {
     const uint64_t rounds = (n_tasks + round - 1) / round;
-    const uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac(QB))) / blocks;
+    uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac(QB))) / blocks;
+    if (rounds / blocks > st + k.steal_max_wg) st = rounds / blocks - k.steal_max_wg; // the cap
     if (st >= kStealAhead && st * blocks < rounds) k.steal_s = (uint32_t)st;
   } else if (dyn && a.steal != nullptr && k.steal_permille > 0) {
     k.steal_s = kStealOnDevice; // device-counted: the kernel sizes the pool from *n_dev

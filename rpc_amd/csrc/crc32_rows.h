@@ -851,7 +851,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if constexpr (!STEAL) return 0u;
     if (a.steal_s != kStealOnDevice) return a.steal_s;
     const uint32_t rounds = (n_tasks + kRound - 1) / kRound;
-    const uint32_t st = (uint32_t)(((uint64_t)rounds * (1000u - a.steal_permille)) / 1000u) / nblk;
+    uint32_t st = (uint32_t)(((uint64_t)rounds * (1000u - a.steal_permille)) / 1000u) / nblk;
+    if (rounds / nblk > st + a.steal_max_wg) st = rounds / nblk - a.steal_max_wg; // (launch_rows' cap)
     return (st >= kStealAhead && st * nblk < rounds) ? st : 0u;
   }();
   const bool steal = STEAL && steal_s != 0u;
