@@ -42,7 +42,7 @@ struct ItemsArgs {
   // steal_s is set by launch_rows.
   uint32_t *steal = nullptr;
   uint32_t steal_s = 0;         // kStealOnDevice: the kernel sizes the pool from the device count
-  uint32_t steal_permille = 150; // pool share of the rounds (steal_s on the device)
+  uint32_t steal_permille = 80;  // pool share of the rounds (steal_s on the device)
   uint32_t steal_max_wg = 48;     // ... at most this many pool rounds per workgroup
   // Words zeroed by workgroup 0 at launch (<= 1024; the contiguous chunk
   // combine XORs into them afterwards).

@@ -230,8 +230,11 @@ static double env_frac(const char *name, double dflt) {
   const double v = e ? atof(e) : dflt;
   return (v >= 0.0 && v < 1.0) ? v : dflt;
 }
+// Round 4 (final tree): 0.08 instead of 0.15 -- NS -1.15 / -0.1 %, C4 -0.7 /
+// -0.9 %, C1 -0.45 % on two boxes, rotated (profiles/r04zi, r04zj); 0.05 was
+// better still for NS / C4 on one box but +1.5 % for C1, 0.03 +1.5-2 % for all.
 static double steal_frac(int QB = 1) {
-  static const double f1 = env_frac("RPCCRC_STEAL_FRAC", 0.15);
+  static const double f1 = env_frac("RPCCRC_STEAL_FRAC", 0.08);
   static const double f4 = env_frac("RPCCRC_STEAL_FRAC_QB4", f1);
   return QB == 4 ? f4 : f1;
 }
