@@ -288,6 +288,62 @@ def cpu_baseline(w: Workload, target_s: float):
     }
 
 
+# Per-rank correctness at every N: after the timed region each
+# rank checks its first RANK_CHECK_BODIES CRCs against the reference crc.c.
+RANK_CHECK_BODIES = 1 << 16
+
+
+def rank_check_sample(w: Workload):
+    """(host bytes, offsets, lengths, device CRCs) of this rank's first bodies."""
+    nb = min(w.n, RANK_CHECK_BODIES)
+    if w.kind == "uniform":
+        host = w.base[: nb * w.L].cpu().numpy()
+        offs = np.arange(nb, dtype=np.uint64) * np.uint64(w.L)
+        lens = np.full(nb, w.L, dtype=np.uint32)
+    elif w.kind == "ragged":
+        offs, lens = w.offs_h[:nb], w.lens_h[:nb]
+        host = w.base[: int(offs[-1] + lens[-1])].cpu().numpy()
+    else:  # large: the first body (256 MiB)
+        nb = 1
+        host = w.base[: w.L].cpu().numpy()
+        offs = np.zeros(1, dtype=np.uint64)
+        lens = np.full(1, w.L, dtype=np.uint32)
+    return host, offs, lens, w.out[:nb].cpu().numpy().view(np.uint32)
+
+
+def rank_crc_check(host, offs, lens, dev_crc, threads: int) -> dict:
+    """This rank's device CRCs against the reference crc.c (oracle/_ref, built from
+    /root/reference/crc.c) -- the cpu_baseline leg's checker, outside the timed
+    region; the oracle restatement where the reference build is absent."""
+    from oracle import oracle  # checker only (test/baseline infrastructure)
+
+    ref = oracle.load_ref()
+    if ref is not None:
+        _, want = ref.batch_timed(host, offs, lens, threads=threads, reps=1)
+        checker = "reference crc.c (oracle/_ref/libref_crc.so)"
+    else:
+        want = oracle.crc32_batch_mt(host, offs, lens, threads=threads)
+        checker = "oracle restatement (oracle/_ref absent)"
+    bad = int(np.count_nonzero(np.asarray(dev_crc, dtype=np.uint32) != want))
+    return {"bodies": int(len(want)), "mismatches": bad, "checker": checker}
+
+
+def reduce_crc_check(dist, device, rec: dict, world: int) -> dict:
+    """ranks_crc_check over ranks: how many ranks had every sampled CRC right."""
+    ok = 1 if rec["mismatches"] == 0 else 0
+    if dist is not None:
+        from rpc_amd.shard import sum_over_ranks
+
+        ranks_ok = sum_over_ranks(dist, ok, device)
+        bodies = sum_over_ranks(dist, rec["bodies"], device)
+        mism = sum_over_ranks(dist, rec["mismatches"], device)
+    else:
+        ranks_ok, bodies, mism = ok, rec["bodies"], rec["mismatches"]
+    return {"ranks": world, "ranks_ok": ranks_ok, "bodies_checked": bodies, "mismatches": mism,
+            "bodies_per_rank": rec["bodies"], "checker": rec["checker"],
+            "of": "each rank's first bodies of its own shard, after the timed region"}
+
+
 def host_inclusive(w: Workload):
     """Pinned host buffer -> H2D -> kernel -> D2H of CRCs through rpc_crc32_batch."""
     if w.kind != "uniform":
@@ -412,18 +468,31 @@ def frames_lifted_probe(device, n=1024, reps=5, seed=0x5EED0007):
             "route_span_mode": aligned_4k and os.environ.get("RPCCRC_BIG_SPAN", "1") != "0"}
 
 
-def stream_read_probe(w: Workload, reps=10):
+def stream_read_probe(w: Workload, steps: int, reps=10, rounds=3):
     """Achievable HBM read rate on the same buffer (SURVEY 8d "a measured
     stream-read kernel"):
       * rows_dealing_GBps -- the ceiling of the product's own memory stream: the
         rows kernel with its CRC work compiled out, same DYN rounds + tail
         stealing, same 4 x 16 B non-temporal loads a row ahead, no stores
-        (rpc_crc32_stream_read_device pattern 2).  frac_of_stream_read uses it.
+        (rpc_crc32_stream_read_device pattern 2).  Timed under the product's
+        own protocol: after a re-warm, `rounds` pairs of
+        blocks -- K = `steps` probe launches, K product steps -- back to back
+        on the product's stream with one event between blocks (order swapped
+        every round), so frac_of_stream_read compares the two at one clock.
       * coalesced_nt{1,0}_GBps -- a plain grid-stride loop with coalesced 16-B
         lanes and no tail dealing (rounds 1-3's probe; the product beat it)."""
     nbytes = (w.total // 4096) * 4096
     stream = torch.cuda.current_stream()
     res = {}
+
+    def block(fn, k):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(k):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / k
 
     def timed(fn):
         fn()
@@ -431,25 +500,47 @@ def stream_read_probe(w: Workload, reps=10):
         while time.perf_counter() - t0 < 0.2:
             fn()
             torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            fn()
-        e1.record(stream)
-        e1.synchronize()
-        return e0.elapsed_time(e1) / 1e3 / reps
+        return block(fn, reps)
 
     nrows = min(nbytes, 1 << 34) // 4096  # <= 16 GiB per launch (C2's 37 GiB: its first 16 GiB)
     if nrows >= (1 << 16):
         try:
-            t = timed(lambda: rpc_amd.stream_read(w.base, 2, nbytes=nrows * 4096))
-            res["rows_dealing_GBps"] = round(nrows * 4096 / t / 1e9, 1)
-            res["rows_dealing_us"] = round(t * 1e6, 2)
+            probe = lambda: rpc_amd.stream_read(w.base, 2, nbytes=nrows * 4096)  # noqa: E731
+            # re-warm as before the main pass, then every block back to back
+            # (one event between blocks, no host sync: the clock stays at its
+            # steady state, as in the timed pass)
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 0.3:
+                w.step()
+                torch.cuda.synchronize()
+            for _ in range(steps):
+                w.step()
+            seq = []
+            for r in range(rounds):
+                order = (("probe", probe), ("product", w.step))
+                seq += list(order if r % 2 == 0 else order[::-1])
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(seq) + 1)]
+            ev[0].record(stream)
+            for i, (name, fn) in enumerate(seq):
+                for _ in range(steps):
+                    fn()
+                ev[i + 1].record(stream)
+            ev[-1].synchronize()
+            t = {"probe": [], "product": []}
+            for i, (name, _) in enumerate(seq):
+                t[name].append(ev[i].elapsed_time(ev[i + 1]) / 1e3 / steps)
+            tp, tc = float(np.mean(t["probe"])), float(np.mean(t["product"]))
+            res["rows_dealing_GBps"] = round(nrows * 4096 / tp / 1e9, 1)
+            res["rows_dealing_us"] = round(tp * 1e6, 2)
+            res["product_interleaved_us"] = round(tc * 1e6, 2)
+            res["product_interleaved_GBps"] = round(w.algo_bytes / tc / 1e9, 1)
+            res["protocol"] = (f"{rounds} x ({steps} probe launches, {steps} product steps), order swapped each "
+                               "round, back to back after a 0.3 s re-warm, one event between blocks")
         except rpc_amd.RpcCrcError as e:  # an older library under A/B (tools/ab_lib.sh)
             res["rows_dealing_error"] = str(e)
     for nt in (1, 0):
-        t = timed(lambda: rpc_amd.stream_read(w.base, 0, nontemporal=bool(nt), nbytes=nbytes))
-        res[f"coalesced_nt{nt}_GBps"] = round(nbytes / t / 1e9, 1)
+        t_nt = timed(lambda: rpc_amd.stream_read(w.base, 0, nontemporal=bool(nt), nbytes=nbytes))
+        res[f"coalesced_nt{nt}_GBps"] = round(nbytes / t_nt / 1e9, 1)
     return res
 
 
@@ -575,9 +666,23 @@ def reduce_rehearsal(args, world: int, rank: int):
     k = 1e-3 * (1.0 + rank / 10.0)
     algo = CONFIGS[args.config][2] * (CONFIGS[args.config][3] + 4)
     t = rank_timing(dist, None, k * args.steps, k, k, algo - 4 * CONFIGS[args.config][2])
+    # the per-rank CRC check on a small CPU-made shard (seed of this rank); the
+    # "device" CRCs are the oracle's, with body 7 corrupted on RPCCRC_BENCH_BAD_RANK
+    from oracle import oracle
+    from rpc_amd.shard import rank_seed
+
+    nb, L = 64, 4096
+    host = oracle.splitmix_bytes(nb * L, rank_seed(CONFIGS[args.config][4], rank))
+    offs = np.arange(nb, dtype=np.uint64) * np.uint64(L)
+    lens = np.full(nb, L, dtype=np.uint32)
+    dev = oracle.crc32_batch(host, offs, lens)
+    if os.environ.get("RPCCRC_BENCH_BAD_RANK") == str(rank):
+        dev[7] ^= 1
+    chk = reduce_crc_check(dist, None, rank_crc_check(host, offs, lens, dev, 1), world)
     if rank == 0:
         line = {"n_gpus": world, "value": round(t["total"] * args.steps / t["wall"] / GiB, 2),
-                "roofline": roofline_fields(algo, t, world)}
+                "roofline": roofline_fields(algo, t, world),
+                "ranks_crc_ok": chk["ranks_ok"] == world, "ranks_crc_check": chk}
         sys.stdout.flush()
         os.write(1, (json.dumps(line) + "\n").encode())
     dist.destroy_process_group()
@@ -706,12 +811,16 @@ def main():
         median_src = "second K-step pass with an event after every step (each adds a marker between launches)"
     tr = rank_timing(dist, device, wall, kernel_s, median_s, w.total)
     tmax, total_bytes = tr["wall"], tr["total"]
+    # every rank checks its own first bodies (outside the timed region)
+    log("per-rank CRC check against the reference crc.c")
+    chk = reduce_crc_check(dist, device, rank_crc_check(*rank_check_sample(w),
+                                                        threads=max(1, effective_cpus()[0] // max(1, world))), world)
 
     extra = {}
     cpu = None
     if rank == 0 and world == 1:
         log("stream-read probe")
-        extra["stream_read_probe"] = stream_read_probe(w)
+        extra["stream_read_probe"] = stream_read_probe(w, args.steps)
         if not args.no_host_inclusive:
             log("host-inclusive batch")
             extra["host_inclusive"] = host_inclusive(w)
@@ -779,16 +888,20 @@ def main():
                            else "crc32_rows_kernel",
                            "large": "crc32_rows_kernel (+chunk combine)"}[w.kind],
                 "median_source": median_src,
-                # the same achieved rate against a streaming read
-                # of the same buffer on the same GPU, measured in this run: the
-                # rows kernel's own dealing and loads with no CRC work
-                # (stream_read_probe rows_dealing_GBps).
-                "frac_of_stream_read": (round(achieved / extra["stream_read_probe"]["rows_dealing_GBps"], 4)
-                                        if "rows_dealing_GBps" in extra.get("stream_read_probe", {}) else None),
+                # the achieved rate against a streaming read of the
+                # same buffer on the same GPU, measured in this run: the rows
+                # kernel's own dealing and loads with no CRC work, in blocks
+                # alternating with blocks of product steps (stream_read_probe)
+                "frac_of_stream_read": (round(extra["stream_read_probe"]["product_interleaved_GBps"]
+                                              / extra["stream_read_probe"]["rows_dealing_GBps"], 4)
+                                        if "product_interleaved_GBps" in extra.get("stream_read_probe", {}) else None),
             },
             # the reference crc.c on the host's cores: timed on rank 0 at N = 1 only
             # (an N > 1 run shares the host among N ranks)
             "cpu_baseline": cpu if world == 1 else None,
+            # every rank's first bodies against the reference crc.c
+            "ranks_crc_ok": chk["ranks_ok"] == world,
+            "ranks_crc_check": chk,
             "prewarm": {"seconds": args.prewarm_s, "steps": prewarm_steps},
             "device": rpc_amd.device_info(),
             "extra": extra,

@@ -733,7 +733,10 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     r.rnd_image = c.img_round;
     if (route_all) {
       r.all_n = (uint32_t)n;
-      if (cmp) {
+      // (the verdicts come from the aligned route's fold only: the end-aligned
+      // fold, big_combine_kernel, writes CRCs -- with RPCCRC_BIG_ALIGNED=0 the
+      // caller's compare launch writes them)
+      if (cmp && g_big_aligned) {
         r.cmp_expected = cmp->expected;
         r.cmp_pre = cmp->pre;
         r.cmp_verdict = cmp->verdict;
@@ -1055,7 +1058,28 @@ bool service_enabled() {
 }
 constexpr uint64_t kSvcIdleTicks = 200000;   // 2 ms without a request (s_memrealtime, 100 MHz)
 constexpr uint64_t kSvcLifeTicks = 2000000;  // 20 ms per instance: bounds what a device-wide sync waits for
-constexpr uint64_t kSvcWaitNs = 2000000000;  // a call that gets no answer in 2 s is a device failure
+// A call with no answer after kSvcWaitNs gives its request up and takes the
+// launch-per-call path instead (VERDICT / ADVICE r04: the service may not be
+// placed while other kernels fill the GPU; that path then waits on its own
+// stream, and surfaces a real device error).  The abandoned request is safe to
+// leave: nobody waits for its seq, and the slot's next request carries a new one.
+constexpr uint64_t kSvcWaitNs = 2000000000;
+
+// Test hook, compiled into the test build only (librpccrc_test.so):
+// RPCCRC_TEST_SVC_MUTE=K makes the next K inline service requests unanswerable
+// (their tag never matches) and their wait 20 ms, to exercise the fallback.
+bool take_test_svc_mute() {
+#ifdef RPCCRC_TEST_HOOKS
+  static std::atomic<long> left{[] {
+    const char *e = getenv("RPCCRC_TEST_SVC_MUTE");
+    return e ? atol(e) : 0L;
+  }()};
+  return left.fetch_sub(1) > 0;
+#else
+  return false;
+#endif
+}
+std::atomic<uint64_t> g_svc_fallbacks{0}; // calls that gave their service request up
 
 std::vector<Service *> g_services; // for the exit handler (under g_services_mu)
 std::mutex g_services_mu;
@@ -1146,10 +1170,12 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
   SvcReq &rq = sh->rq[slot];
   uint32_t q = ++v.seq[slot];
   if (q == 0) q = ++v.seq[slot]; // 0: the answered seq of a fresh slot
+  const bool mute = len <= kSvcInline && take_test_svc_mute();
+  const uint64_t wait_ns = mute ? 20000000ull : kSvcWaitNs;
   if (len <= kSvcInline) { // in the request block, ending at its inline byte 116; then line 1's tag
     memcpy(rq.inl + kSvcInline - len, src, len);
     std::atomic_thread_fence(std::memory_order_release);
-    *reinterpret_cast<volatile uint32_t *>(&rq.tag) = q;
+    *reinterpret_cast<volatile uint32_t *>(&rq.tag) = mute ? q ^ 0x80000000u : q;
   } else {
     const uint32_t seg = svc::seg_of(len);
     memcpy(sh->body[slot] + 64u * seg - len, src, len);
@@ -1170,7 +1196,11 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
           ok = false;
           break;
         }
-        if ((spin & 4095u) == 0 && mono_ns() - t0 > kSvcWaitNs) die("drop-in service (no answer)", RPCCRC_EIO);
+        if ((spin & 4095u) == 0 && mono_ns() - t0 > wait_ns) { // give the request up (above)
+          g_svc_fallbacks.fetch_add(1, std::memory_order_relaxed);
+          ok = false;
+          break;
+        }
       }
     }
   }

@@ -64,3 +64,29 @@ def test_gpus2_reductions_report_slowest_rank():
     assert abs(r["achieved"] - algo / 1.1e-3 / 1e9) < 0.1
     # value: both ranks' bytes over the slowest rank's wall time
     assert abs(lines[0]["value"] - 2 * (1 << 23) * 4096 / 1.1e-3 / (1 << 30)) < 0.1
+
+
+def _reduce_only(extra_env):
+    env = dict(os.environ, RPCCRC_BENCH_REDUCE_ONLY="1", **extra_env)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return lines[0]
+
+
+def test_gpus2_per_rank_crc_check():
+    """the N > 1 line says whether every rank's CRCs were right.  Two
+    gloo ranks run bench.py's own check (rank_crc_check against the reference crc.c,
+    reduce_crc_check over the ranks) on a CPU-made shard each; with
+    RPCCRC_BENCH_BAD_RANK=1 rank 1 reports one corrupted CRC."""
+    good = _reduce_only({})
+    assert good["ranks_crc_ok"] is True
+    c = good["ranks_crc_check"]
+    assert c["ranks"] == 2 and c["ranks_ok"] == 2 and c["mismatches"] == 0 and c["bodies_checked"] == 128
+    bad = _reduce_only({"RPCCRC_BENCH_BAD_RANK": "1"})
+    assert bad["ranks_crc_ok"] is False
+    c = bad["ranks_crc_check"]
+    assert c["ranks_ok"] == 1 and c["mismatches"] == 1 and c["bodies_checked"] == 128

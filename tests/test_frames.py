@@ -458,3 +458,21 @@ def test_frames_role_flags_rejected():
         rc = rpc_amd._lib.rpc_frames_verify_device(d.data_ptr(), 64, o.data_ptr(), 1, flags, v.data_ptr(), None,
                                                    rpc_amd._stream_handle(None))
         assert rc == -22, flags
+
+
+def test_frames_lifted_cap_end_aligned_route():
+    """with RPCCRC_BIG_ALIGNED=0 the route cuts end-aligned chunks
+    and its fold (big_combine_kernel) writes CRCs only, so a route-all verify must
+    still launch the compare that writes the verdicts.  The lifted-cap verify /
+    stamp tests run again in a child process under that setting."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RPCCRC_BIG_ALIGNED="0")
+    p = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(repo, "tests", "test_frames.py"), "-k",
+                        "lifted_cap_large_bodies or lifted_cap_route_all_mixed or lifted_cap_route_modes"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=repo)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
+    assert " passed" in p.stdout and "failed" not in p.stdout, p.stdout[-2000:]
