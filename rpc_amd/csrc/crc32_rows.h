@@ -684,6 +684,20 @@ constexpr uint32_t kStealAhead = RPCCRC_STEAL_AHEAD;
 #endif
 constexpr uint32_t kStealClaimAt = RPCCRC_STEAL_CLAIM_AT;
 constexpr uint32_t kStealQ = 16;                      // LDS queue ring
+// Queue capacity.  A wave that grabbed its next task (one ahead) in pool round
+// R maps it to a queue entry only at its next item switch; meanwhile the other
+// waves can start tasks up to round R + kDynSlots (the output ring stops them
+// only at their OUTPUT) and claim kStealAhead rounds past that.  Entry R of
+// the ring must not be overwritten by then, or the lagging wave never finds
+// its claim: it spins until its wait cap, its round is never stored, and every
+// wave waiting for that ring slot caps too (RPCCRC_EIO).  That is what failed
+// in round 4's pool-UNIT variant (RPCCRC_STEAL_SPLIT, profiles/r04b/split_ab.txt):
+// units of 1/2 or 1/4 round made the lead 2 or 4 times as many queue entries
+// (~20 or ~40 against 16) while the whole-round pool's lead is ~10 (DESIGN.md
+// 4.1).  Rebuilt in round 5 with a queue sized for it, the units passed every
+// test and still ran slower (C1 +4 %, NS +1.5 %, profiles/r05d).
+static_assert(kStealQ >= dyn_slots(1) + kStealAhead + 2 && kStealQ >= dyn_slots(4) + kStealAhead + 2,
+              "steal queue shorter than the rounds a workgroup can run ahead of a lagging wave");
 constexpr uint32_t kStealCtlWords = 3 + 2 * kStealQ;  // tail, done, inflight, tags[Q], ids[Q]
 // Bounded waits.  Both waits end by protocol (a claim is published by the wave
 // holding it at the end of its current row, before it waits on anything, and
