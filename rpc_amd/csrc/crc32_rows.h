@@ -394,6 +394,10 @@ constexpr int kRowsAblNtStore = 2048; // non-temporal CRC stores (DYN paths; exa
 // the instruction cost of a half-width row (timing only: wrong CRCs).
 constexpr int kRowsAblHalfChain = 8192;
 constexpr int kRowsAblNoSub = 16384; // ragged QB = 1 without the quarter / half first rows (exact)
+// Ragged QB = 1 lane-Horner pipeline (the C2 loop: loads two rows ahead) with
+// the chain, the per-lane Horner and the merge replaced by an XOR fold: its
+// memory stream and control path alone (timing only: wrong CRCs).
+constexpr int kRowsAblPipeMem = 65536;
 // Feature bit (product, not an ablation): uniform QB = 1 DYN launches of
 // 4096-byte RAW items also store each whole round's crc0 -- the 32 items as one
 // 128 KiB run -- at a.round_out[round] (rpc_crc32_device_large's contiguous
@@ -1347,7 +1351,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // -0.2 % against -0.5 % here, profiles/r03p)
 #define RPCCRC_CHAIN_ONLY(cb, ch)                                                        \
   do {                                                                                   \
-    if (kSub && c_r == 0 && c_lp <= kQuarter) {                                          \
+    if constexpr ((ABL & kRowsAblPipeMem) != 0) {                                        \
+      ch = xor_fold(cb);                                                                 \
+    } else if (kSub && c_r == 0 && c_lp <= kQuarter) {                                   \
       ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
     } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
       ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
@@ -1359,6 +1365,18 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   } while (0)
     auto lane_horner_p = [&](bool ok, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed, uint32_t cidx,
                              uint32_t tsk, uint32_t chain) {
+      if constexpr ((ABL & kRowsAblPipeMem) != 0) {
+        lacc = (r != 0 ? lacc : seed) ^ chain;
+        if (r + 1 == nr) {
+          const uint32_t res = (uint32_t)__builtin_amdgcn_readfirstlane((int)lacc);
+          if constexpr (DYN) {
+            if (ok) dyn_out(cidx, tsk, res);
+          } else {
+            if (ok) park(res);
+          }
+        }
+        return;
+      }
       if (r != 0) {
         lacc = rw_map(lds, lacc) ^ chain;
       } else { // a body's first row starts the accumulator (zlib's seed in lane 63)

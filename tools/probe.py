@@ -243,7 +243,8 @@ def ragged_ablate(a):
     out = torch.empty(w.n, dtype=torch.int32, device=w.device)
     s = torch.cuda.current_stream()
     names = {0: "product", 16384: "full first rows (no sub-rows)", 3: "memory only", 4: "compute only",
-             16: "no stores", 2: "no merge", 19: "memory only, no stores"}
+             16: "no stores", 2: "no merge", 19: "memory only, no stores",
+             65536: "memory + control of the product's pipeline (XOR fold)"}
     if a.only:
         names = {k: v for k, v in names.items() if str(k) in a.only.split(",")}
 

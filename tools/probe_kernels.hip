@@ -133,6 +133,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_ragged(const ui
   case 16: go_ragged<16>(a, blocks, s); break;
   case 2: go_ragged<2>(a, blocks, s); break;
   case 3 | 16: go_ragged<3 | 16>(a, blocks, s); break;
+  case kRowsAblPipeMem: go_ragged<kRowsAblPipeMem>(a, blocks, s); break;
   default: return -22;
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
