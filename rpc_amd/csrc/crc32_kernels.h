@@ -184,17 +184,30 @@ constexpr uint32_t kSvcInline = 116;                   // bodies up to this leng
 //   line 0: req = {len (low), seq (high)}, then inline bytes 0..55
 //   line 1: inline bytes 56..115, then tag
 // An inline body (len <= kSvcInline) ends at inline byte 116, so its CRC needs no
-// second PCIe round trip; longer bodies go to SvcShared::body.  Each line is read
-// whole (one cache line), but the two lines of one poll in no set order: the
-// host writes the bytes, then line 1's tag (= the request's seq), then line 0's
-// req word, and the service takes an inline request only when the tag matches
-// its seq (a line read whole shows a prefix of the host's stores to it).
+// second PCIe round trip; longer bodies go to SvcShared::body.  The host writes
+// the bytes, then line 1's tag, then line 0's req word; the service takes an
+// inline request only when the XOR of the block's 32 dwords -- len, seq, the
+// 29 inline words, the tag -- is 0, i.e. the tag equals svc_tag(len, seq,
+// inline words).  A poll's dwords (one per lane) come back in pieces of the
+// memory system's choosing, in no set order; a poll that caught any piece
+// before the host's stores to it (a stale word next to a current req word, in
+// either line) shows a non-zero XOR with probability 1 - 2^-32 unless the stale
+// words equal the new ones, and is retried (round 4's tag checked
+// line 1 only, and relied on line 0 being read as one 64-B snapshot).
+// Rounds 1-4 took the tag = seq.
 struct SvcReq {
   uint64_t req;
   uint8_t inl[kSvcInline];
   uint32_t tag;
 };
 static_assert(sizeof(SvcReq) == 128, "two lines per request block");
+static_assert(kSvcInline % 4 == 0, "inline bytes as whole words");
+// The tag of an inline request (host side; the service checks the XOR).
+inline uint32_t svc_tag(uint32_t len, uint32_t seq, const uint32_t *inl_words) {
+  uint32_t x = len ^ seq;
+  for (uint32_t k = 0; k < kSvcInline / 4; ++k) x ^= inl_words[k];
+  return x;
+}
 struct SvcShared {
   // one block per slot (a shared line was written by up to 8 caller threads
   // while 8 waves polled it: 10 callers took 30 us a call, r04c)

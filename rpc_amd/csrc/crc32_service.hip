@@ -12,20 +12,22 @@
 // Protocol (SvcShared, hipHostMallocCoherent: every access below bypasses the
 // GPU caches -- sc0 sc1 loads / stores, no cache-wide fence):
 //   host   writes a body of <= kSvcInline bytes into the slot's request block
-//          (SvcReq: the tag, then the bytes, ending at inline byte 116), a
+//          (SvcReq: the bytes, ending at inline byte 116, then the tag), a
 //          longer one right-aligned into body[slot] (virtual buffer of 64 * seg
 //          bytes, seg = 4 / 8 / 16 bytes per lane by length), then
 //          rq[slot].req = {len, seq} as ONE 64-bit store (x86 stores stay in order);
 //   wave   polls the request blocks of its kSvcPer slots (one dword per lane,
 //          both blocks in one round trip); a seq it has not answered is a
-//          request (inline: once the block's tag equals it).  An inline body is
+//          request (inline: once the XOR of the block's dwords is 0, i.e.
+//          the tag matches every word polled -- SvcReq).  An inline body is
 //          already in registers; a longer one is read (every lane its seg bytes;
 //          the loads of all its pending slots in flight together).  It computes
 //          the CRC and stores {crc, seq} into res[slot] (one 64-bit store);
 //   host   spins on res[slot] until the seq matches.
 // The waves share the time of the last request in LDS (4 bytes) and all leave
 // after idle_ticks without one, after the kernel's lifetime cap, or when the
-// host sets ctl[kSvcStop]; the last wave out stores its instance number into
+// host sets ctl[kSvcStop] -- together: the first wave to decide sets s_leave,
+// which every wave checks before each poll; the last wave out stores its instance number into
 // ctl[kSvcExited], so the host knows when to launch a new instance (a request
 // that arrives while an instance is leaving is picked up by the next one:
 // pending = seq not yet answered in res).
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     uint32_t instance) {
   __shared__ uint32_t s_last;  // low 32 bits of the last request's s_memrealtime
   __shared__ uint32_t s_alive; // waves still in the loop
+  __shared__ uint32_t s_leave; // set by the first wave that decides to leave: all leave
   // Tq of the inline lengths: an LDS read instead of a dependent global load per
   // request (476 B of LDS still fits beside any rows workgroup: <= 163040 B)
   __shared__ uint32_t s_tq[kSvcInline + 1];
@@ -117,6 +120,7 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
   if (threadIdx.x == 0) {
     s_last = (uint32_t)t_start;
     s_alive = kSvcWaves;
+    s_leave = 0u;
   }
   for (uint32_t k = threadIdx.x; k <= kSvcInline; k += 64 * kSvcWaves) s_tq[k] = tq[k];
   __syncthreads();
@@ -138,7 +142,20 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
   // byte v - 132, so lane L's word is block dword L - 33 (lanes >= 33).
   const int src0 = (int)lane - 33;
   for (uint32_t poll = 0;; ++poll) {
+    // one wave decided to leave: all leave together (a wave that stayed would
+    // keep the instance alive while the departed wave's slots went unanswered)
+    if (__hip_atomic_load(&s_leave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
     const uint32_t pv = ld_sys32(pblk); // both blocks, one round trip
+    // XOR of each block's 32 dwords (lanes 32 i .. 32 i + 31): 0 for a whole,
+    // current inline request (crc32_kernels.h SvcReq)
+    uint32_t xs = pv ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)pv, 0xB1, 0xF, 0xF, true); // quad_perm [1,0,3,2]
+    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x4E, 0xF, 0xF, true);              // quad_perm [2,3,0,1]
+    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x124, 0xF, 0xF, true);             // row_ror:4
+    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x128, 0xF, 0xF, true);             // row_ror:8
+    {
+      const auto sw = __builtin_amdgcn_permlane16_swap(xs, xs, false, false); // lane bit 4
+      xs = sw[0] ^ sw[1];
+    }
     uint32_t lens[kSvcPer], seqs[kSvcPer];
     bool pend[kSvcPer], inl[kSvcPer];
     bool any = false;
@@ -146,11 +163,11 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     for (uint32_t i = 0; i < kSvcPer; ++i) {
       lens[i] = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 0));
       seqs[i] = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 1));
-      const uint32_t tag = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 31));
+      const uint32_t xsum = (uint32_t)__builtin_amdgcn_readlane((int)xs, (int)(32 * i));
       if (lens[i] > kSvcMaxLen) lens[i] = kSvcMaxLen; // (the host never sends more)
       inl[i] = lens[i] <= kSvcInline;
-      // an inline request counts once its block's second line (tag) is current
-      pend[i] = seqs[i] != served[i] && (!inl[i] || tag == seqs[i]);
+      // an inline request counts once the whole block is current (XOR 0)
+      pend[i] = seqs[i] != served[i] && (!inl[i] || xsum == 0u);
       any = any || pend[i];
     }
     if (any) {
@@ -190,7 +207,10 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     const uint32_t last = __hip_atomic_load(&s_last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     bool leave = (uint32_t)now - last > (uint32_t)idle_ticks || now - t_start > life_ticks;
     if ((poll & 63u) == 63u) leave = leave || ld_sys32(&sh->ctl[kSvcStop]) != 0u;
-    if (leave) break;
+    if (leave) {
+      if (lane == 0) __hip_atomic_store(&s_leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
   // the last wave out tells the host this instance is gone (a vector store)

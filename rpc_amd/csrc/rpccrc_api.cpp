@@ -313,6 +313,10 @@ struct Service {
   // A thread first tries the slot it held last (the same wave, k % kSvcWaves).
   std::atomic<uint32_t> busy{0};
   uint32_t seq[kSvcSlots] = {}; // last request seq of each slot (written by the slot's holder)
+  // Host copy of each slot's inline bytes (kSvcInline, as the request block holds
+  // them): the tag's checksum covers all of them (svc_tag), and reading them back
+  // from the coherent (uncached) block would cost a PCIe-speed read per word.
+  uint32_t inl[kSvcSlots][kSvcInline / 4] = {};
   bool ok = false;
 };
 
@@ -1173,9 +1177,12 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
   const bool mute = len <= kSvcInline && take_test_svc_mute();
   const uint64_t wait_ns = mute ? 20000000ull : kSvcWaitNs;
   if (len <= kSvcInline) { // in the request block, ending at its inline byte 116; then line 1's tag
+    uint8_t *shadow = reinterpret_cast<uint8_t *>(v.inl[slot]);
+    memcpy(shadow + kSvcInline - len, src, len);
     memcpy(rq.inl + kSvcInline - len, src, len);
     std::atomic_thread_fence(std::memory_order_release);
-    *reinterpret_cast<volatile uint32_t *>(&rq.tag) = mute ? q ^ 0x80000000u : q;
+    const uint32_t tag = svc_tag(len, q, v.inl[slot]);
+    *reinterpret_cast<volatile uint32_t *>(&rq.tag) = mute ? tag ^ 0x80000000u : tag;
   } else {
     const uint32_t seg = svc::seg_of(len);
     memcpy(sh->body[slot] + 64u * seg - len, src, len);
