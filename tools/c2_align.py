@@ -55,6 +55,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", type=int, default=0)
     ap.add_argument("--n", type=int, default=1 << 22)
+    ap.add_argument("--abl", type=int, default=-1,
+                    help="time tools/libprobe.so's ragged rows kernel with these ablation bits instead of the "
+                         "product (65536: the product's pipeline with an XOR fold -- memory + control only)")
+    ap.add_argument("--uniform4k", action="store_true", help="also a layout of 4 KiB bodies (same bytes) as a ragged batch")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     lens = _loguniform_lengths(a.n, 0x5EED0004)
@@ -72,9 +76,31 @@ def main():
         print(f"c2_align: layout {A}: {total} B", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
 
+    if a.uniform4k:  # the same byte count cut into 4 KiB bodies, 4 KiB-aligned, passed as a ragged batch
+        n4 = int(lens.sum(dtype=np.uint64)) // 4096
+        buf = torch.empty(n4 * 4096, dtype=torch.uint8, device=dev)
+        rpc_amd.fill_random(buf, 0x5EED0404)
+        o4 = torch.from_numpy((np.arange(n4, dtype=np.uint64) * np.uint64(4096)).view(np.int64)).to(dev)
+        l4 = torch.full((n4,), 4096, dtype=torch.int32, device=dev)
+        lays[4096] = (buf, o4, torch.empty(n4, dtype=torch.int32, device=dev), n4 * 4096, l4)
+        aligns.append(4096)
+    probe = None
+    if a.abl >= 0:
+        import ctypes
+        probe = ctypes.CDLL(os.path.join(REPO, "tools", "libprobe.so"))
+        probe.probe_rows_ragged.restype = ctypes.c_int
+        probe.probe_rows_ragged.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+
     def step(A):
-        buf, d_offs, out, _ = lays[A]
-        rpc_amd.device_batch(buf, d_offs, d_lens, out=out, max_len=65536)
+        buf, d_offs, out, _ = lays[A][:4]
+        dl = lays[A][4] if len(lays[A]) > 4 else d_lens
+        if probe is not None:
+            rc = probe.probe_rows_ragged(buf.data_ptr(), d_offs.data_ptr(), dl.data_ptr(), d_offs.numel(),
+                                         out.data_ptr(), a.abl, 256, torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, rc
+        else:
+            rpc_amd.device_batch(buf, d_offs, dl, out=out, max_len=65536)
 
     if a.only:
         for _ in range(a.reps):
@@ -103,7 +129,7 @@ def main():
     summary = {str(A): {"us": [round(x, 1) for x in v], "min_us": round(min(v), 1),
                         "frac_best": round(algo / min(v) / 8e6, 4), "span_bytes": lays[A][3]}
                for A, v in res.items()}
-    print(json.dumps({"algo_bytes": algo, "layouts": summary}), flush=True)
+    print(json.dumps({"algo_bytes": algo, "abl": a.abl, "layouts": summary}), flush=True)
 
 
 if __name__ == "__main__":
