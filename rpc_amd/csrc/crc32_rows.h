@@ -424,6 +424,16 @@ constexpr bool kSubRows = RPCCRC_SUBROWS != 0;
 #define RPCCRC_LANE_HORNER 1
 #endif
 constexpr bool kLaneHorner = RPCCRC_LANE_HORNER != 0;
+// Ragged DYN QB = 1: tasks are groups of 4 items, and the group's items that
+// fit a 1 KiB quarter share one row (round 5, crc32_rows_kernel kSB).  Exact
+// (82 ragged / frames GPU tests green with it, profiles/r05m) but C2 ran 11 %
+// SLOWER (6784 vs 6115 us, rotated A/B on one box): the extra row kind and the
+// group state in the three unrolled pipeline steps took the kernel from 10 to
+// 56 SGPR spills (~160 v_readlane per step) -- more than the 1.2M row steps it
+// saves.  Off; kept as the measured alternative.
+#ifndef RPCCRC_SMALL_GROUPS
+#define RPCCRC_SMALL_GROUPS 0
+#endif
 // Ragged QB = 1: an item's offset and length loads issued together, then one
 // wait (round 4).  The compiler had sunk the offset load below the length's
 // route test: two serial scalar-load round trips per item (ISA).
@@ -747,6 +757,9 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   constexpr bool kSub = kSubRows && QB == 1 && RAGGED && !kTwoChains &&
                         (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose | kRowsAblHalfChain | kRowsAblNoSub)) == 0;
   constexpr uint32_t kImgBytes = kSub ? kLdsBytesV3 : kLdsBytesV2;
+  // Ragged DYN QB = 1 (the C2 path): small items four per row (see kSB's loop)
+  constexpr bool kSB = RPCCRC_SMALL_GROUPS != 0 && QB == 1 && RAGGED && DYN && !STEAL && DEPTH == 1 && kSub &&
+                       kLaneHorner && kRowsPipe && kRaggedAhead2 && (ABL & ~kRowsAblNoStore) == 0;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kImgBytes / 4];
   // DYN control block (dyn_ring_words): task counter, done counts, slot
   // generations (slot s starts at round s), CRC ring.
@@ -834,7 +847,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if constexpr ((ABL & kRowsAblNtStore) != 0) __builtin_nontemporal_store(v, p);
     else *p = v;
   };
-  const uint32_t n_tasks = (QB == 4) ? (n + 3) / 4 : n;
+  const uint32_t n_tasks = (QB == 4 || kSB) ? (n + 3) / 4 : n; // (kSB: groups of 4 items)
   // Group dealing, G = 2^a.gshift: in each whole round of nwaves * G tasks,
   // wave gw takes the G consecutive tasks [gw * G, gw * G + G), so its results
   // of a round are G consecutive outputs (G = 32: the wave writes whole 128-B
@@ -1235,6 +1248,306 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       finish(valid, len, z, nr, r, seed, cidx, tsk, m);
     };
 
+    if constexpr (kSB) {
+      // ---- small-body groups (kSB, round 5) ----
+      // Tasks are groups of 4 consecutive items.  The items of a group whose
+      // end-padded length fits a 1 KiB quarter ("small") share ONE row, one
+      // quarter each, computed as a QB = 4 row (P row); the group's other
+      // items take their own rows as before (sub-row heads, lane Horner).
+      // C2's 1.67M small bodies cost ~420 us of its ~6.2 ms as one row each
+      // (tools/c2_subsets.py, profiles/r05j).  Each wave keeps its group's 4
+      // CRCs in lanes 0..3 of `gres` and stores them (4 lanes, 16 B) once the
+      // group's last row is merged -- no output ring (a group's rows are one
+      // wave's, in order).
+      const uint32_t ngroups = n_tasks;
+      auto item_ol = [&](uint32_t item, uint64_t &off, uint32_t &len) __attribute__((always_inline)) { // (meta()'s loads and routing)
+        off = ld_const(a.offsets, item);
+        len = ld_const(a.lengths, item);
+        if constexpr (kMetaCoissue) __asm__ volatile("" : "+s"(off), "+s"(len));
+        if (len >= a.big_min && a.routed != nullptr) {
+          const uint32_t bi = a.out_idx ? ld_const(a.out_idx, item) : item;
+          if ((ld_const(a.routed, bi >> 5) >> (bi & 31u)) & 1u) len = 0;
+        }
+      };
+      // generator (the producer of stage-m rows): its group, that group's small
+      // items (P row) and items with rows of their own (bit b = item 4g + b)
+      uint32_t gg = first_task, gsm = 0, gns = 0, gdone = 0;
+      uint32_t pend = 0;
+      // P row of a group: one descriptor at B (the first small item's 16-B
+      // block); quarter b reads item b's 1 KiB window at per-lane offsets
+      // d_b + pofs, pieces wholly before the item (pofs + 16 <= front_b) none.
+      // (four named scalars each, not arrays: an array a lambda captures by
+      // reference went to scratch, and its values to VGPRs -- "illegal VGPR to
+      // SGPR copy" for the descriptor base)
+      struct Q4 {
+        uint32_t v0, v1, v2, v3;
+        __device__ uint32_t get(uint32_t b) const { return b == 0 ? v0 : b == 1 ? v1 : b == 2 ? v2 : v3; }
+        __device__ void set(uint32_t b, uint32_t x) {
+          if (b == 0) v0 = x;
+          else if (b == 1) v1 = x;
+          else if (b == 2) v2 = x;
+          else v3 = x;
+        }
+      };
+      uint64_t pB = 0;
+      Q4 pd{0, 0, 0, 0}, pfront{kQuarter, kQuarter, kQuarter, kQuarter};
+      uint32_t plzA = 0, plzB = 0;
+      // one small-item candidate b: fills its P-row quarter or marks it for rows of its own
+      auto classify = [&](uint32_t g, uint32_t b) __attribute__((always_inline)) {
+        // (no early returns: the compiler merged `gns |= ` / `gsm |= ` on
+        // different paths into a store through a pointer phi -- both went to
+        // scratch)
+        const bool exists = 4u * g + b < n;
+        uint64_t off = 0;
+        uint32_t len = 0;
+        if (exists) item_ol(4u * g + b, off, len);
+        const uint64_t p = (uint64_t)(uintptr_t)a.base + off;
+        const uint32_t zb = (uint32_t)(0u - (uint32_t)(p + len)) & 15u;
+        const bool fits = exists && len + zb <= kQuarter;
+        const uint64_t B = (gsm == 0u) ? (p & ~(uint64_t)15) : pB; // the first small item's 16-B block
+        const uint64_t rel = p - B; // items outside [B, B + 1 GiB - 2048) take rows of their own
+        const bool small = fits && (rel >> 30) == 0u && (uint32_t)rel < (1u << 30) - 2048u;
+        if (small && gsm == 0u) pB = B;
+        const uint32_t bit = 1u << b;
+        gsm |= small ? bit : 0u;
+        gns |= (exists && !small) ? bit : 0u;
+        if (small && len != 0u) { // (an empty item: no loads, lz = 0 -> CRC 0 by the algebra)
+          pfront.set(b, kQuarter - len - zb);
+          pd.set(b, (uint32_t)rel + len + zb - kQuarter);
+          const uint32_t lz = (len << 4) | zb;
+          if (b < 2) plzA |= lz << (16u * b);
+          else plzB |= lz << (16u * (b - 2u));
+        }
+      };
+      auto load_group = [&](uint32_t g) __attribute__((always_inline)) {
+        gsm = gns = 0;
+        plzA = plzB = 0;
+        pd = Q4{0, 0, 0, 0};
+        pfront = Q4{kQuarter, kQuarter, kQuarter, kQuarter};
+        classify(g, 0);
+        classify(g, 1);
+        classify(g, 2);
+        classify(g, 3);
+      };
+      // Rows through the pipeline: (item, r, nr, lp, len, z, seed, p0).
+      //   item rows: nr >= 1, lp = hd | kGLast on the group's last row.
+      //   P rows:    nr = 0, item = 4g, lp = the small mask | kGLast, len / z
+      //              = the packed lz words (lz = len << 4 | z, 16 bits each).
+      //   invalid:   nr = kNone (past the wave's last group; loads from safe_sb).
+      // (No separate ok / flag fields: every SGPR counts -- an earlier version
+      // spilled 129 SGPRs and ran 11 % slower, profiles/r05l.)
+      constexpr uint32_t kGLast = 0x80000000u, kNone = 0xFFFFFFFFu;
+      auto gen = [&](uint32_t pitem, uint32_t pr, uint32_t pnr, uint64_t pp0, uint32_t plp, uint32_t plen,
+                     uint32_t pz, uint32_t pseed, uint32_t &item, uint32_t &r, uint32_t &nr, uint64_t &p0,
+                     uint32_t &lp, uint32_t &len, uint32_t &z, uint32_t &seed) __attribute__((always_inline)) {
+        item = pitem;
+        p0 = pp0;
+        len = plen;
+        z = pz;
+        seed = pseed;
+        r = 0;
+        if (pnr != kNone && pnr != 0u && pr + 1u < pnr) { // the item's next row (metadata reused)
+          r = pr + 1u;
+          nr = pnr;
+          const uint32_t b = pitem & 3u;
+          lp = (plp & ~kGLast) | ((r + 1u == nr && (gns >> (b + 1u)) == 0u) ? kGLast : 0u);
+          return;
+        }
+        uint32_t rest = 0;
+        if (pnr != kNone) rest = (pnr == 0u) ? gns : (gns & ~((2u << (pitem & 3u)) - 1u));
+        nr = kNone;
+        lp = 0;
+        if (rest == 0u && gdone == 0u) { // the next group
+          const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+          gg = dyn_task(c);
+          if (gg < ngroups) {
+            pend = dyn_grab();
+            load_group(gg);
+            rest = gns;
+            if (gsm != 0u) { // its P row
+              item = 4u * gg;
+              nr = 0;
+              p0 = pB;
+              lp = gsm | ((gns == 0u) ? kGLast : 0u);
+              len = plzA;
+              z = plzB;
+              return;
+            }
+          } else {
+            gdone = 1;
+          }
+        }
+        if (rest == 0u) return; // nothing left: an invalid row
+        const uint32_t b = (uint32_t)__builtin_ctz(rest);
+        item = 4u * gg + b;
+        meta(item, p0, lp, len, z, nr, seed);
+        lp |= (nr == 1u && (gns >> (b + 1u)) == 0u) ? kGLast : 0u;
+      };
+      uint64_t safe_sb = 0; // 16-B block of this wave's first bytes: invalid rows load from it
+      auto issue_sb = [&](uint64_t p0, uint32_t lp, uint32_t nr, uint32_t r, u32x4 (&buf)[4]) __attribute__((always_inline)) {
+        // one load sequence (see issue): whole rows, P rows, first / invalid rows
+        const uint32_t hd = lp & ~kGLast;
+        uint64_t base;
+        uint32_t off[4];
+        if (nr != kNone && nr != 0u && !(r == 0u && hd < kRow)) {
+          base = p0 + (uint64_t)r * kRow + hd - kRow;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) off[b] = pofs + b * kQuarter;
+        } else if (nr == 0u) {
+          base = p0;
+#pragma unroll
+          for (uint32_t b = 0; b < 4; ++b) off[b] = (pofs + 16u > pfront.get(b)) ? pd.get(b) + pofs : kOobOffset;
+        } else {
+          const bool ok = nr != kNone;
+          base = ok ? (p0 & ~(uint64_t)15) : safe_sb;
+          const int32_t d = ok ? (int32_t)(r * kRow + hd) - (int32_t)kRow + (int32_t)(p0 & 15) : INT32_MIN / 2;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) off[b] = min((uint32_t)(d + (int32_t)(pofs + b * kQuarter)), kOobOffset);
+        }
+        const __amdgpu_buffer_rsrc_t row = row_rsrc(base);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row, off[b]);
+      };
+      // A P row, all of it (stage c): per 16-lane row hi its item's CRC, valid
+      // in lanes 4..7 -- QB = 4's algebra (fix, chain, merge step 1, zlib seed
+      // A_{len+z}(F) = ZI_{up-q}(TQ16[up / 16]) with q = len + z, ZI_z, ~).
+      auto p_row = [&](uint32_t lzA, uint32_t lzB, u32x4 (&cb)[4]) __attribute__((always_inline)) -> uint32_t {
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+          const uint32_t lz = ((b < 2u ? lzA : lzB) >> (16u * (b & 1u))) & 0xFFFFu;
+          const uint32_t len_b = lz >> 4, z_b = lz & 15u;
+          if (len_b != 0u) fix_quarter<false>(cb[b], lane, kQuarter - len_b - z_b, z_b);
+        }
+        transpose(cb);
+        const uint32_t ch = row_quarters(lds, cb, lsel, lsel1, upper);
+        const uint32_t lzr = ((hi < 2u ? lzA : lzB) >> (16u * (hi & 1u))) & 0xFFFFu;
+        const uint32_t q = (lzr >> 4) + (lzr & 15u), up = (q + 15u) & ~15u, zq = up - q, zl = lzr & 15u;
+        uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
+        {
+          const uint32_t nib = (w >> dl.shift) & 15u;
+          const uint32_t t = dist_reduce8(lds_ld(lds, kLdsZI2 + (zq != 0u ? zq - 1u : 0u) * 512u + dl.n64 + nib * 4u));
+          // lanes 4..7 / 12..15 of each row hold the row's value; row_shl:4 brings it to 0..3 / 8..11
+          const uint32_t tb = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x104, 0xF, 0xF, true);
+          w = (zq != 0u) ? ((lane & 4u) ? t : tb) : w;
+        }
+        uint32_t res = ch ^ ((mode == kModeRaw) ? 0u : w);
+        {
+          const uint32_t nib = (res >> dl.shift) & 15u;
+          const uint32_t t = dist_reduce8(lds_ld(lds, kLdsZI2 + (zl != 0u ? zl - 1u : 0u) * 512u + dl.n64 + nib * 4u));
+          res = (zl != 0u) ? t : res; // valid in lanes 4..7 of each row
+        }
+        return (mode == kModeFinal) ? ~res : res;
+      };
+      uint32_t lacc = 0, gres = 0;
+      // stage p: a P row's CRCs into gres, or an item row's lane-Horner step
+      // (its CRC on its last row); the group's CRCs stored on its last row
+      auto retire = [&](uint32_t item, uint32_t r, uint32_t nr, uint32_t lp, uint32_t z, uint32_t seed,
+                        uint32_t chain) __attribute__((always_inline)) {
+        if (nr == kNone) return;
+        if (nr == 0u) {
+          const uint32_t v = (uint32_t)__shfl((int)chain, (int)(16u * (lane & 3u) + 4u), 64);
+          if (lane < 4u && ((lp >> lane) & 1u) != 0u) gres = v;
+        } else {
+          if (r != 0u) {
+            lacc = rw_map(lds, lacc) ^ chain;
+          } else { // a body's first row starts the accumulator (zlib's seed in lane 63)
+            lacc = chain ^ ((lane == 63u) ? seed : 0u);
+          }
+          if (r + 1u == nr) {
+            const RowMerge m = merge_row(lds, merge_lo(lds, lacc, lsel1), 0u, dl);
+            uint32_t res = m.crc;
+            if (z != 0u) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
+            if (mode == kModeFinal) res = ~res;
+            if (lane == (item & 3u)) gres = res;
+          }
+        }
+        if ((lp & kGLast) != 0u) { // the group's last row: its CRCs, 4 lanes
+          const uint32_t it = (item & ~3u) + lane;
+          if constexpr ((ABL & kRowsAblNoStore) == 0) {
+            if (lane < 4u && it < n) store_out(a.out + oidx(it), gres);
+          } else {
+            sink ^= gres;
+          }
+        }
+      };
+      uint32_t c_item = 0, c_r = 0, c_nr = kNone, c_lp = 0, c_len = 0, c_z = 0, c_seed = 0;
+      uint32_t n_item, n_r, n_nr, n_lp, n_len, n_z, n_seed;
+      uint32_t p_item = 0, p_r = 0, p_nr = kNone, p_lp = 0, p_z = 0, p_seed = 0, p_chain = 0;
+      uint64_t c_p0 = 0, n_p0;
+      // the first group (gg = first_task): its first row
+      load_group(gg);
+      gdone = 0;
+      if (gsm != 0u) {
+        c_item = 4u * gg;
+        c_nr = 0;
+        c_p0 = pB;
+        c_lp = gsm | ((gns == 0u) ? kGLast : 0u);
+        c_len = plzA;
+        c_z = plzB;
+      } else {
+        const uint32_t b = (uint32_t)__builtin_ctz(gns);
+        c_item = 4u * gg + b;
+        meta(c_item, c_p0, c_lp, c_len, c_z, c_nr, c_seed);
+        c_lp |= (c_nr == 1u && (gns >> (b + 1u)) == 0u) ? kGLast : 0u;
+      }
+      safe_sb = c_p0 & ~(uint64_t)15;
+      u32x4 bufA[4], bufB[4], bufC[4];
+      issue_sb(c_p0, c_lp, c_nr, c_r, bufA);
+      if constexpr (kEarly) RPCCRC_ROWS_BEGIN();
+      pend = dyn_grab();
+      gen(c_item, c_r, c_nr, c_p0, c_lp, c_len, c_z, c_seed, n_item, n_r, n_nr, n_p0, n_lp, n_len, n_z, n_seed);
+      issue_sb(n_p0, n_lp, n_nr, n_r, bufB);
+      auto step = [&](u32x4 (&cb)[4], u32x4 (&mb)[4]) __attribute__((always_inline)) {
+        uint32_t m_item, m_r, m_nr, m_lp, m_len, m_z, m_seed;
+        uint64_t m_p0;
+        gen(n_item, n_r, n_nr, n_p0, n_lp, n_len, n_z, n_seed, m_item, m_r, m_nr, m_p0, m_lp, m_len, m_z, m_seed);
+        issue_sb(m_p0, m_lp, m_nr, m_r, mb);
+        uint32_t ch;
+        const uint32_t c_hd = c_lp & ~kGLast;
+        if (c_nr == 0u) { // P row: four small items, one per quarter (QB = 4 row)
+          ch = p_row(c_len, c_z, cb);
+        } else {
+          fix_row(c_hd, c_z, c_nr, c_r, cb);
+          if (c_r == 0 && c_hd <= kQuarter) {
+            ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);
+          } else if (c_r == 0 && c_hd <= 2 * kQuarter) {
+            ch = half_row_segs(lds, cb, lsel, sub_mu);
+          } else {
+            transpose(cb);
+            ch = seg_crc(lds, cb, lsel);
+          }
+        }
+        retire(p_item, p_r, p_nr, p_lp, p_z, p_seed, p_chain);
+        p_item = c_item;
+        p_r = c_r;
+        p_nr = c_nr;
+        p_lp = c_lp;
+        p_z = c_z;
+        p_seed = c_seed;
+        p_chain = ch;
+        c_item = n_item;
+        c_r = n_r;
+        c_nr = n_nr;
+        c_p0 = n_p0;
+        c_lp = n_lp;
+        c_len = n_len;
+        c_z = n_z;
+        c_seed = n_seed;
+        n_item = m_item;
+        n_r = m_r;
+        n_nr = m_nr;
+        n_p0 = m_p0;
+        n_lp = m_lp;
+        n_len = m_len;
+        n_z = m_z;
+        n_seed = m_seed;
+      };
+      do {
+        step(bufA, bufC);
+        step(bufB, bufA);
+        step(bufC, bufB);
+      } while (p_nr != kNone);
+    } else {
     uint32_t c_item = first_task;
     uint64_t c_p0;
     uint32_t c_lp, c_len, c_z, c_nr, c_seed, c_r = 0; // c_lp: the item's first-row bytes (hd)
@@ -1608,6 +1921,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         step(bufC, bufB);
       } while (c_ok);
     }
+    } // (!kSB)
     publish();
     flush();
     if constexpr ((ABL & kRowsAblNoStore) != 0)
