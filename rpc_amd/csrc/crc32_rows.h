@@ -131,16 +131,23 @@ static_assert(kOobOffset >= kRsrcRange, "the out-of-range offset must fail the r
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(uint64_t base) {
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)kRsrcRange, 0x00020000);
 }
+// Cache-policy bits of the non-temporal row loads (the builtin's aux operand;
+// 2 = nt).  RPCCRC_ROW_AUX overrides them for A/B builds only: sc0|nt, sc1|nt
+// and sc0|sc1|nt measured the same as nt on NS and C2, sc1 alone +11 % / +6 %
+// (profiles/r05n/row_load_cache_policy_ab.txt).
+#ifndef RPCCRC_ROW_AUX
+#define RPCCRC_ROW_AUX 2
+#endif
 template <bool NT>
 __device__ __forceinline__ u32x4 ldb16(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, NT ? 2 : 0);
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, NT ? RPCCRC_ROW_AUX : 0);
 }
 // A 16-B piece at signed offset `off` from a uniform base; pieces with off < 0
 // (before the data) are not read at all and come back as zeros: their offset
 // is replaced by one past the descriptor's range (raw buffer range check).
 template <bool NT>
 __device__ __forceinline__ u32x4 ldb16_or_zero(__amdgpu_buffer_rsrc_t rsrc, int32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)min((uint32_t)off, kOobOffset), 0, NT ? 2 : 0);
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)min((uint32_t)off, kOobOffset), 0, NT ? RPCCRC_ROW_AUX : 0);
 }
 
 // Edge fix of one quarter of 16-B pieces (replaces a per-lane byte mask of
