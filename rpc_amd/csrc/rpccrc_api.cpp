@@ -350,6 +350,12 @@ struct DeviceCtx {
   StealPool *steal = nullptr;
   Service *svc = nullptr;       // built on the first drop-in call (svc_once)
   std::once_flag svc_once;
+  // The stream-read probe's output sink (its kernel stores nothing that is
+  // read): one device block for the context, not a workspace lease per call --
+  // a lease orders itself after the block's last use with an event wait, a
+  // gap between back-to-back probe launches the product's launches do not have.
+  uint32_t *probe_sink = nullptr;
+  std::once_flag probe_once;
 };
 
 DeviceCtx g_dev[kMaxDevices];
@@ -1567,10 +1573,17 @@ int rpc_crc32_stream_read_device(const void *d_src, uint64_t nbytes, int pattern
     StealLease sl;
     if ((rc = sl.get(*c, n, 1, s))) return rc;
     if (!sl.p) return RPCCRC_EINVAL; // too small to deal dynamically
-    Lease sink;
-    if ((rc = sink.get(c->ws, 16 * 4 * (size_t)max_blocks_for(*c), s))) return rc;
+    std::call_once(c->probe_once, [c] {
+      int prev = 0;
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(c->device);
+      void *p = nullptr; // one uint32 per wave of a full grid (kRowsAblNoStore writes at most a.out[gw])
+      if (hipMalloc(&p, 16 * 4 * 8 * (size_t)std::max(c->cus, 256)) == hipSuccess) c->probe_sink = static_cast<uint32_t *>(p);
+      (void)hipSetDevice(prev);
+    });
+    if (!c->probe_sink) return RPCCRC_ENOMEM;
     ItemsArgs a = items_args(*c, static_cast<const uint8_t *>(d_src), nullptr, nullptr, n, 4096, 4096, kModeFinal,
-                             reinterpret_cast<uint32_t *>(sink.ptr()));
+                             c->probe_sink);
     a.steal = sl.p;
     return map_hip(launch_stream_rows(a, max_blocks_for(*c), s, sl.done_event(), &sl.recorded));
   }
