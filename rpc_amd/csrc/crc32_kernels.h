@@ -311,6 +311,11 @@ struct SplitLists {
 hipError_t split_workspace_bytes(uint64_t n, size_t *bytes);
 hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes, bool nt, int max_blocks,
                               hipStream_t stream);
+// Small bodies only (len + end pad <= 1 KiB each; crc32_small.h), CRC i to
+// out[out_idx[i]] (out_idx non-null) or out[i]; the count from *n_dev when set
+// (n_items: its upper bound).
+hipError_t launch_small(const ItemsArgs &a, bool nt, int max_blocks, hipStream_t stream);
+bool small_kernel_on();
 hipError_t launch_splitmix_fill(void *dst, uint64_t nbytes, uint64_t seed, hipStream_t stream);
 hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool nt, int max_blocks, uint32_t *out,
                               hipStream_t stream);

@@ -26,6 +26,7 @@
 #include "crc32_kernels.h"
 #include "crc32_layout.h"
 #include "crc32_packed.h"
+#include "crc32_small.h"
 #include "crc32_rows.h"
 #include "frames.h"
 #include "../../include/rpccrc.h"
@@ -534,6 +535,33 @@ hipError_t split_scan(void *tmp, size_t &bytes, const uint32_t *flag, uint32_t *
 }
 } // namespace
 
+// The small-body kernel (crc32_small.h) for split lists; RPCCRC_SMALL_KERNEL=0
+// restores the rows kernel's QB = 4 loop (A/B).
+bool small_kernel_on() {
+  static const bool on = [] {
+    const char *e = getenv("RPCCRC_SMALL_KERNEL");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
+hipError_t launch_small(const ItemsArgs &a, bool nt, int max_blocks, hipStream_t s) {
+  if (a.n_items == 0) return hipSuccess;
+  if (a.offsets == nullptr || a.lengths == nullptr || a.n_items > kMaxLaunchItems) return hipErrorInvalidValue;
+  // every wave at least a few iterations of 16 bodies
+  const uint64_t want = (a.n_items + 16 * 16 * 4 - 1) / (16 * 16 * 4);
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)max_blocks));
+  const dim3 grid((unsigned)blocks), block(kBlock);
+#define RPCCRC_SMALL(N, I) hipLaunchKernelGGL((crc32_small_kernel<N, I>), grid, block, 0, s, a)
+  if (nt) {
+    if (a.out_idx) RPCCRC_SMALL(true, true); else RPCCRC_SMALL(true, false);
+  } else {
+    if (a.out_idx) RPCCRC_SMALL(false, true); else RPCCRC_SMALL(false, false);
+  }
+#undef RPCCRC_SMALL
+  return hipGetLastError();
+}
+
 hipError_t split_workspace_bytes(uint64_t n, size_t *bytes) {
   size_t scan = 0;
   const hipError_t e = split_scan(nullptr, scan, nullptr, nullptr, n, nullptr);
@@ -580,7 +608,7 @@ hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes,
   a.lengths = l.s_len;
   a.n_dev = l.counts;
   a.out_idx = l.s_idx;
-  e = launch_rows(a, 4, nt, max_blocks, s);
+  e = small_kernel_on() ? launch_small(a, nt, max_blocks, s) : launch_rows(a, 4, nt, max_blocks, s);
   if (e != hipSuccess) return e;
   a.offsets = l.b_off; // the rest, one body per row sequence
   a.lengths = l.b_len;

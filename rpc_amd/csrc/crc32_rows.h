@@ -1934,7 +1934,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     if constexpr ((ABL & kRowsAblNoStore) != 0)
       if (sink == 0x9E3779B9u) a.out[gw] = sink; // keeps the results live
     if constexpr ((ABL & kRowsAblTimes) != 0) {
-      uint64_t *times = const_cast<uint64_t *>(a.offsets);
+      // (ragged batches need their offsets: the probe passes the times array in round_out)
+      uint64_t *times = RAGGED ? reinterpret_cast<uint64_t *>(a.round_out) : const_cast<uint64_t *>(a.offsets);
       const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
       if (lane == 0) {
         times[4 * gw + 0] = t_entry;
@@ -2236,7 +2237,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     publish();
     flush();
     if constexpr ((ABL & kRowsAblTimes) != 0) {
-      uint64_t *times = const_cast<uint64_t *>(a.offsets);
+      // (ragged batches need their offsets: the probe passes the times array in round_out)
+      uint64_t *times = RAGGED ? reinterpret_cast<uint64_t *>(a.round_out) : const_cast<uint64_t *>(a.offsets);
       const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
       if (lane == 0) {
         times[4 * gw + 0] = t_entry;

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """tools/pmc_mix.py -- per-launch PMC counters of the rows kernel (median over
 dispatches) from rocprofv3 --pmc CSV directories; divides by a row count.
-Usage: python tools/pmc_mix.py <rows_per_launch> <dir> [<dir> ...]"""
+Usage: python tools/pmc_mix.py <rows_per_launch> <dir> [<dir> ...]
+(PMC_KERNEL=<name substring> selects another kernel.)"""
 import csv
 import glob
 import json
@@ -17,7 +18,7 @@ def main():
         per = {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if "crc32_rows_kernel" not in r["Kernel_Name"]:
+                if os.environ.get("PMC_KERNEL", "crc32_rows_kernel") not in r["Kernel_Name"]:
                     continue
                 per.setdefault(r["Counter_Name"], {}).setdefault((f, r["Dispatch_Id"]), 0.0)
                 per[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])

@@ -125,16 +125,25 @@ def timeline(w, a):
     lib.probe_rows_times.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                      ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p,
                                                                                ctypes.c_int]
-    qb = 4 if w.L <= 1024 else 1
+    ragged = w.kind == "ragged"
+    qb = 1 if ragged else (4 if w.L <= 1024 else 1)
     nw = 256 * 16
     times = torch.zeros(nw * 4, dtype=torch.int64, device=w.device)
     out = torch.empty(w.n, dtype=torch.int32, device=w.device)
     s = torch.cuda.current_stream()
+    if ragged:  # the C2 path: ragged QB = 1, DYN (static rounds, as the product)
+        lib.probe_rows_ragged_times.restype = ctypes.c_int
+        lib.probe_rows_ragged_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
 
     def f():
-        rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1,
-                                  512 | (1024 if a.dyn or a.steal else 0) | (4096 if a.steal else 0), 1, 256,
-                                  s.cuda_stream, times.data_ptr(), a.gshift)
+        if ragged:
+            rc = lib.probe_rows_ragged_times(w.base.data_ptr(), w.offs.data_ptr(), w.lens.data_ptr(), w.n,
+                                             out.data_ptr(), 256, s.cuda_stream, times.data_ptr())
+        else:
+            rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1,
+                                      512 | (1024 if a.dyn or a.steal else 0) | (4096 if a.steal else 0), 1, 256,
+                                      s.cuda_stream, times.data_ptr(), a.gshift)
         assert rc == 0, rc
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:

@@ -139,6 +139,31 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_ragged(const ui
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// The same kernel with the per-wave timeline (kRowsAblTimes; exact results):
+// d_times (4 words per wave) travels in round_out, unused by ragged batches.
+extern "C" __attribute__((visibility("default"))) int probe_rows_ragged_times(const uint8_t *d_base, const uint64_t *d_offs,
+                                                                               const uint32_t *d_lens, uint64_t n,
+                                                                               uint32_t *d_out, int blocks, void *stream,
+                                                                               uint64_t *d_times) {
+  if (ensure_tables()) return -12;
+  ItemsArgs a;
+  a.base = d_base;
+  a.offsets = d_offs;
+  a.lengths = d_lens;
+  a.n_items = n;
+  a.stride = 0;
+  a.len = 0;
+  a.mode = kModeFinal;
+  a.lds_image = g_img;
+  a.tq = g_tq;
+  a.out = d_out;
+  a.gshift = 0;
+  a.round_out = reinterpret_cast<uint32_t *>(d_times);
+  hipLaunchKernelGGL((crc32_rows_kernel<1, true, true, kRowsAblTimes, 1, true>), dim3(blocks), dim3(1024), 0,
+                     static_cast<hipStream_t>(stream), a);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 // ---------------------------------------------------------------------------
 // Row-shape stream probes (MEASUREMENT ONLY): does a wave-iteration cost track
 // the bytes it reads or the load instructions it issues?  Tile t of TB bytes
