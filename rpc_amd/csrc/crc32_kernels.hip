@@ -234,10 +234,18 @@ static double env_frac(const char *name, double dflt) {
 // Round 4 (final tree): 0.08 instead of 0.15 -- NS -1.15 / -0.1 %, C4 -0.7 /
 // -0.9 %, C1 -0.45 % on two boxes, rotated (profiles/r04zi, r04zj); 0.05 was
 // better still for NS / C4 on one box but +1.5 % for C1, 0.03 +1.5-2 % for all.
-static double steal_frac(int QB = 1) {
+// Ragged QB = 1 launches (C2) take a smaller pool (RPCCRC_STEAL_FRAC_RAGGED):
+// with the two-phase loop their pool rounds still cost ~30 % more than static
+// ones (the protocol at every item switch; a C2 item averages 2.6 rows), so
+// the pool is sized to the exit spread it absorbs (~6 % without a pool,
+// profiles/r05v) and no larger: C2 rotated A/B on one box, no pool 6073 / 6100
+// / 6102 us, 2 % 6069 / 6078 / 6087, 3 % 6041 / 6048 / 6069, 5 % 6052 / 6076 /
+// 6079, 8 % 6046 / 6064 / 6066 (profiles/r05x, r05z).
+static double steal_frac(int QB = 1, bool ragged = false) {
   static const double f1 = env_frac("RPCCRC_STEAL_FRAC", 0.08);
   static const double f4 = env_frac("RPCCRC_STEAL_FRAC_QB4", f1);
-  return QB == 4 ? f4 : f1;
+  static const double fr = env_frac("RPCCRC_STEAL_FRAC_RAGGED", 0.03);
+  return QB == 4 ? f4 : ragged ? fr : f1;
 }
 // ... but at most this many pool rounds per workgroup: the pool has to absorb
 // the workgroups' spread in finishing time, not a share of an ever larger
@@ -298,11 +306,11 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // rounds go to the device-counter pool, the rest stay static per workgroup.
   ItemsArgs k = a;
   k.steal_s = 0;
-  k.steal_permille = (uint32_t)(steal_frac(QB) * 1000.0 + 0.5);
+  k.steal_permille = (uint32_t)(steal_frac(QB, ragged) * 1000.0 + 0.5);
   k.steal_max_wg = steal_max_per_wg();
   if (dyn && a.steal != nullptr && a.n_dev == nullptr) {
     const uint64_t rounds = (n_tasks + round - 1) / round;
-    uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac(QB))) / blocks;
+    uint64_t st = (uint64_t)((double)rounds * (1.0 - steal_frac(QB, ragged))) / blocks;
     if (rounds / blocks > st + k.steal_max_wg) st = rounds / blocks - k.steal_max_wg; // the cap
     if (st >= kStealAhead && st * blocks < rounds) k.steal_s = (uint32_t)st;
   } else if (dyn && a.steal != nullptr && k.steal_permille > 0) {

@@ -1555,379 +1555,412 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         step(bufC, bufB);
       } while (p_nr != kNone);
     } else {
-    uint32_t c_item = first_task;
-    uint64_t c_p0;
-    uint32_t c_lp, c_len, c_z, c_nr, c_seed, c_r = 0; // c_lp: the item's first-row bytes (hd)
-    meta(c_item, c_p0, c_lp, c_len, c_z, c_nr, c_seed);
-    const uint64_t safe = c_p0 & ~(uint64_t)15; // 16-B block holding this wave's first byte
-    // Successor of task (item, r) with metadata nr: same item next row, or the
-    // wave's next item.  Invalid successors carry the wave's first item's
-    // (in-range) metadata and load from `safe`; their results are dropped.
+    // Stealing launches run in two phases (round 5): phase 1 -- the loop
+    // compiled WITHOUT the pool protocol -- takes the static rounds up to the
+    // one whose first task claims from the pool; phase 2 (the full protocol)
+    // starts from the task phase 1 grabbed last and takes the rest.  The pool
+    // bookkeeping in the item switch (claims, queue lookups, publishing) then
+    // costs only the last ~8 % of a launch: in one loop it made the ragged
+    // (C2) kernel's loop 30 % larger and C2 1.8 % slower with stealing than
+    // without (profiles/r05w), so C2 ran without it and its exit spread, 380
+    // us (odd XCDs ~130 us behind even ones, profiles/r05v), stayed.
     uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
-    // After the first row's loads: the image / barrier (kEarly), then the grab
-    // of the task after the first one.
-#define RPCCRC_ROWS_START()                        \
-  do {                                             \
-    if constexpr (kEarly) RPCCRC_ROWS_BEGIN();     \
-    if constexpr (DYN) pend = dyn_grab();          \
-  } while (0)
-    uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
-    // more: the wave may still get work (stealing: a task past n inside a
-    // pool round is skipped, not the end).  Invalid rows take one step each.
-    // cur_*: the current row's item metadata, reused for the item's next row
-    // (RAGGED: no reload of its offset / length -- a scalar-load wait in
-    // front of every row's loads otherwise).
-    auto succ = [&](bool ok, bool more, uint32_t item, uint32_t r, uint32_t nr, uint32_t &s_item, uint32_t &s_r,
-                    bool &s_ok, bool &s_more, uint64_t &p0, uint32_t &lp, uint32_t &len, uint32_t &z,
-                    uint32_t &snr, uint32_t &seed, uint64_t cur_p0, uint32_t cur_lp, uint32_t cur_len,
-                    uint32_t cur_z, uint32_t cur_seed) {
-      const bool adv = r + 1 < nr;
-      if constexpr (STEAL) {
-        if (adv) {
-          s_item = item;
-          m_c = c_c;
-          // (`ok && s_item < n`, though implied by ok: written as `ok` it made
-          // the compiler treat the row base as divergent -- a waterfall loop
-          // around every buffer load, ISA)
-          s_ok = ok && s_item < n;
-          s_more = more;
-        } else {
-          s_item = n;
-          s_more = false;
-          if (more) {
-            m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-            claim_if_first(m_c);
-            s_item = dyn_map(m_c, s_more);
-            if (s_more) pend = dyn_grab();
-          }
-          s_ok = s_more && s_item < n;
-        }
-      } else {
-        if constexpr (DYN) {
+    const uint32_t p1_lim = steal ? (steal_s - kStealAhead) * kRound : 0xFFFFFFFFu;
+    auto rows_phase = [&](auto ph) {
+      constexpr int kPh = decltype(ph)::value; // 1: plain loop (all of a launch without a pool), 2: pool phase
+      constexpr bool kS = STEAL && kPh == 2;   // the pool protocol compiled in
+      uint32_t c_item = first_task;
+      uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
+      // more: the wave may still get work (stealing: a task past n inside a
+      // pool round is skipped, not the end).  Invalid rows take one step each.
+      bool c_ok = true, c_more = true;
+      if constexpr (kPh == 2) { // phase 2 starts at the task phase 1 grabbed and left
+        c_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+        claim_if_first(c_c);
+        bool more = false;
+        const uint32_t t0 = dyn_map(c_c, more);
+        more = __builtin_amdgcn_readfirstlane((int)more) != 0;
+        c_more = more;
+        c_ok = more && t0 < n;
+        if (c_ok) c_item = t0; // (else the first task's metadata: an in-range address)
+        if (more) pend = dyn_grab();
+      }
+      uint64_t c_p0;
+      uint32_t c_lp, c_len, c_z, c_nr, c_seed, c_r = 0; // c_lp: the item's first-row bytes (hd)
+      meta(c_item, c_p0, c_lp, c_len, c_z, c_nr, c_seed);
+      const uint64_t safe = c_p0 & ~(uint64_t)15; // 16-B block holding this wave's first byte
+      // Successor of task (item, r) with metadata nr: same item next row, or the
+      // wave's next item.  Invalid successors carry the wave's first item's
+      // (in-range) metadata and load from `safe`; their results are dropped.
+      // After the first row's loads: the image / barrier (kEarly), then the grab
+      // of the task after the first one (phase 2 has done both).
+#define RPCCRC_ROWS_START()                          \
+    do {                                               \
+      if constexpr (kPh != 2) {                        \
+        if constexpr (kEarly) RPCCRC_ROWS_BEGIN();     \
+        if constexpr (DYN) pend = dyn_grab();          \
+      }                                                \
+    } while (0)
+      // cur_*: the current row's item metadata, reused for the item's next row
+      // (RAGGED: no reload of its offset / length -- a scalar-load wait in
+      // front of every row's loads otherwise).
+      auto succ = [&](bool ok, bool more, uint32_t item, uint32_t r, uint32_t nr, uint32_t &s_item, uint32_t &s_r,
+                      bool &s_ok, bool &s_more, uint64_t &p0, uint32_t &lp, uint32_t &len, uint32_t &z,
+                      uint32_t &snr, uint32_t &seed, uint64_t cur_p0, uint32_t cur_lp, uint32_t cur_len,
+                      uint32_t cur_z, uint32_t cur_seed) {
+        const bool adv = r + 1 < nr;
+        if constexpr (kS) {
           if (adv) {
             s_item = item;
             m_c = c_c;
+            // (`ok && s_item < n`, though implied by ok: written as `ok` it made
+            // the compiler treat the row base as divergent -- a waterfall loop
+            // around every buffer load, ISA)
+            s_ok = ok && s_item < n;
+            s_more = more;
           } else {
-            m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-            s_item = dyn_task(m_c);
-            if (ok && s_item < n) pend = dyn_grab(); // no more grabs once the wave is done
+            s_item = n;
+            s_more = false;
+            if (more) {
+              m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+              claim_if_first(m_c);
+              s_item = dyn_map(m_c, s_more);
+              if (s_more) pend = dyn_grab();
+            }
+            s_ok = s_more && s_item < n;
           }
         } else {
-          s_item = adv ? item : next_task(item);
+          if constexpr (DYN) {
+            if (adv) {
+              s_item = item;
+              m_c = c_c;
+            } else {
+              m_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+              s_item = dyn_task(m_c);
+              // phase 1 of a stealing launch ends at the rounds that claim or
+              // come from the pool: that task (left in pend) starts phase 2
+              if constexpr (STEAL) if (m_c >= p1_lim) s_item = n;
+              if (ok && s_item < n) pend = dyn_grab(); // no more grabs once the wave is done
+            }
+          } else {
+            s_item = adv ? item : next_task(item);
+          }
+          s_ok = ok && s_item < n;
+          s_more = s_ok;
         }
-        s_ok = ok && s_item < n;
-        s_more = s_ok;
-      }
-      if (kRowsMetaReuse && RAGGED && adv) {
-        p0 = cur_p0;
-        lp = cur_lp;
-        len = cur_len;
-        z = cur_z;
-        snr = nr;
-        seed = cur_seed;
-      } else {
-        meta(s_ok ? s_item : first_task, p0, lp, len, z, snr, seed);
-      }
-      if (steal && !s_ok) snr = 1u;
-      s_r = adv ? r + 1 : 0u;
-    };
-    // The unrolled loops have ONE exit, at the bottom: a mid-body break edge
-    // (structurized back through the loop header) would carry the first
-    // half's in-flight prefetch into the header, and the compiler would then
-    // drain vmcnt before every prefetch (measured: rows fully serialised on
-    // half the iterations).  Trailing steps past the wave's last task run on
-    // invalid tasks (c_ok false): safe loads, no result parked.
-    bool c_ok = true, c_more = true;
-    // Ragged batches only: C2 -1.6 %, while uniform batches (north star
-    // +-0.5 %, C4's chunks +0.6 %) keep the plain loop
-    // (profiles/r02/r02r_rows_pipeline_ab.txt).
-    constexpr bool kPipe = kRowsPipe && RAGGED && !kTwoChains &&
-                           (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose)) == 0;
-    // Row C's chain (full / half / quarter row, rows::*_row_segs) and row P's
-    // merge, inside each arm so the scheduler overlaps it with C's chain (P's
-    // merge before or after the arms: C2 +1.3 % with the max-ilp scheduler,
-    // profiles/r03m).
+        if (kRowsMetaReuse && RAGGED && adv) {
+          p0 = cur_p0;
+          lp = cur_lp;
+          len = cur_len;
+          z = cur_z;
+          snr = nr;
+          seed = cur_seed;
+        } else {
+          meta(s_ok ? s_item : first_task, p0, lp, len, z, snr, seed);
+        }
+        if (steal && !s_ok) snr = 1u;
+        s_r = adv ? r + 1 : 0u;
+      };
+      // The unrolled loops have ONE exit, at the bottom: a mid-body break edge
+      // (structurized back through the loop header) would carry the first
+      // half's in-flight prefetch into the header, and the compiler would then
+      // drain vmcnt before every prefetch (measured: rows fully serialised on
+      // half the iterations).  Trailing steps past the wave's last task run on
+      // invalid tasks (c_ok false): safe loads, no result parked.
+      // Ragged batches only: C2 -1.6 %, while uniform batches (north star
+      // +-0.5 %, C4's chunks +0.6 %) keep the plain loop
+      // (profiles/r02/r02r_rows_pipeline_ab.txt).
+      constexpr bool kPipe = kRowsPipe && RAGGED && !kTwoChains &&
+                             (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose)) == 0;
+      // Row C's chain (full / half / quarter row, rows::*_row_segs) and row P's
+      // merge, inside each arm so the scheduler overlaps it with C's chain (P's
+      // merge before or after the arms: C2 +1.3 % with the max-ilp scheduler,
+      // profiles/r03m).
 #define RPCCRC_CHAIN_MERGE(cb, ch, pm)                                                   \
-  do {                                                                                   \
-    if (kSub && c_r == 0 && c_lp <= kQuarter) {                                          \
-      ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
-      pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
-    } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
-      ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
-      pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
-    } else {                                                                             \
-      transpose(cb);                                                                     \
-      ch = seg_crc(lds, cb, lsel);                                                       \
-      pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
-    }                                                                                    \
-  } while (0)
-    // Lane Horner (kLH): C's chain only, then row P joins its body's per-lane
-    // accumulator (A_4096 on every row but the first; zlib's seed enters in
-    // lane 63, whose merge shift is A_0), and the body's last row is merged
-    // once: crc0(body) = XOR_L' A_{64(63-L')}(acc_L').
-    constexpr bool kLH = kLaneHorner && kSub;
-    uint32_t lacc = 0; // kLH: this wave's per-lane accumulator of row P's body
-    // (row P's lane-Horner step after C's arms: inside each arm measured
-    // -0.2 % against -0.5 % here, profiles/r03p)
+    do {                                                                                   \
+      if (kSub && c_r == 0 && c_lp <= kQuarter) {                                          \
+        ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
+        pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
+      } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
+        ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
+        pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
+      } else {                                                                             \
+        transpose(cb);                                                                     \
+        ch = seg_crc(lds, cb, lsel);                                                       \
+        pm = merge_row(lds, merge_lo(lds, p_chain, lsel1), W, dl);                         \
+      }                                                                                    \
+    } while (0)
+      // Lane Horner (kLH): C's chain only, then row P joins its body's per-lane
+      // accumulator (A_4096 on every row but the first; zlib's seed enters in
+      // lane 63, whose merge shift is A_0), and the body's last row is merged
+      // once: crc0(body) = XOR_L' A_{64(63-L')}(acc_L').
+      constexpr bool kLH = kLaneHorner && kSub;
+      uint32_t lacc = 0; // kLH: this wave's per-lane accumulator of row P's body
+      // (row P's lane-Horner step after C's arms: inside each arm measured
+      // -0.2 % against -0.5 % here, profiles/r03p)
 #define RPCCRC_CHAIN_ONLY(cb, ch)                                                        \
-  do {                                                                                   \
-    if constexpr ((ABL & kRowsAblPipeMem) != 0) {                                        \
-      ch = xor_fold(cb);                                                                 \
-    } else if (kSub && c_r == 0 && c_lp <= kQuarter) {                                   \
-      ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
-    } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
-      ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
-    } else {                                                                             \
-      transpose(cb);                                                                     \
-      ch = seg_crc(lds, cb, lsel);                                                       \
-    }                                                                                    \
-    lane_horner_p(p_ok, p_z, p_nr, p_r, p_seed, p_c, p_item, p_chain);                   \
-  } while (0)
-    auto lane_horner_p = [&](bool ok, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed, uint32_t cidx,
-                             uint32_t tsk, uint32_t chain) {
-      if constexpr ((ABL & kRowsAblPipeMem) != 0) {
-        lacc = (r != 0 ? lacc : seed) ^ chain;
+    do {                                                                                   \
+      if constexpr ((ABL & kRowsAblPipeMem) != 0) {                                        \
+        ch = xor_fold(cb);                                                                 \
+      } else if (kSub && c_r == 0 && c_lp <= kQuarter) {                                   \
+        ch = quarter_row_segs(lds, cb, lsel, sub_jbq, sub_m3);                             \
+      } else if (kSub && c_r == 0 && c_lp <= 2 * kQuarter) {                               \
+        ch = half_row_segs(lds, cb, lsel, sub_mu);                                         \
+      } else {                                                                             \
+        transpose(cb);                                                                     \
+        ch = seg_crc(lds, cb, lsel);                                                       \
+      }                                                                                    \
+      lane_horner_p(p_ok, p_z, p_nr, p_r, p_seed, p_c, p_item, p_chain);                   \
+    } while (0)
+      auto lane_horner_p = [&](bool ok, uint32_t z, uint32_t nr, uint32_t r, uint32_t seed, uint32_t cidx,
+                               uint32_t tsk, uint32_t chain) {
+        if constexpr ((ABL & kRowsAblPipeMem) != 0) {
+          lacc = (r != 0 ? lacc : seed) ^ chain;
+          if (r + 1 == nr) {
+            const uint32_t res = (uint32_t)__builtin_amdgcn_readfirstlane((int)lacc);
+            if constexpr (DYN) {
+              if (ok) dyn_out(cidx, tsk, res);
+            } else {
+              if (ok) park(res);
+            }
+          }
+          return;
+        }
+        if (r != 0) {
+          lacc = rw_map(lds, lacc) ^ chain;
+        } else { // a body's first row starts the accumulator (zlib's seed in lane 63)
+          if constexpr (kLdsSeed) { // seed holds hd: A_hd(F) = ZI_{up - hd}(TQ16[up / 16])
+            const uint32_t up = (seed + 15u) & ~15u;
+            uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
+            if (up != seed) w = dist_uniform(lds, w, kLdsZI2 + (up - seed - 1u) * 512u, dl);
+            seed = (mode == kModeRaw) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
+          }
+          lacc = chain ^ ((lane == 63u) ? seed : 0u);
+        }
         if (r + 1 == nr) {
-          const uint32_t res = (uint32_t)__builtin_amdgcn_readfirstlane((int)lacc);
+          const RowMerge m = merge_row(lds, merge_lo(lds, lacc, lsel1), 0u, dl);
+          uint32_t res = m.crc;
+          if (z != 0) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
+          if (mode == kModeFinal) res = ~res;
           if constexpr (DYN) {
             if (ok) dyn_out(cidx, tsk, res);
           } else {
             if (ok) park(res);
           }
         }
-        return;
-      }
-      if (r != 0) {
-        lacc = rw_map(lds, lacc) ^ chain;
-      } else { // a body's first row starts the accumulator (zlib's seed in lane 63)
-        if constexpr (kLdsSeed) { // seed holds hd: A_hd(F) = ZI_{up - hd}(TQ16[up / 16])
-          const uint32_t up = (seed + 15u) & ~15u;
-          uint32_t w = lds_ld(lds, kLdsTQ16 + up / 4u);
-          if (up != seed) w = dist_uniform(lds, w, kLdsZI2 + (up - seed - 1u) * 512u, dl);
-          seed = (mode == kModeRaw) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
-        }
-        lacc = chain ^ ((lane == 63u) ? seed : 0u);
-      }
-      if (r + 1 == nr) {
-        const RowMerge m = merge_row(lds, merge_lo(lds, lacc, lsel1), 0u, dl);
-        uint32_t res = m.crc;
-        if (z != 0) res = dist_uniform(lds, res, kLdsZI2 + (z - 1u) * 512u, dl);
-        if (mode == kModeFinal) res = ~res;
-        if constexpr (DYN) {
-          if (ok) dyn_out(cidx, tsk, res);
-        } else {
-          if (ok) park(res);
-        }
+      };
+      if constexpr (DEPTH == 1 && kPipe && kRaggedAhead2) {
+        // The pipeline below with loads two rows ahead: one step issues row M's
+        // loads while row N's (the row after C) are in flight, chains row C and
+        // merges row P.  A wave then keeps a row of loads in flight while it
+        // computes, also across item switches (C2's memory-only variant runs
+        // 5.79 ms against 6.33 for the product with one row ahead).
+        u32x4 bufA[4], bufB[4], bufC[4];
+        issue(c_p0, c_lp, c_nr, c_r, c_ok, safe, bufA);
+        RPCCRC_ROWS_START();
+        uint32_t n_item, n_lp, n_r, n_len, n_z, n_nr, n_seed, n_c;
+        uint64_t n_p0;
+        bool n_ok, n_more;
+        succ(c_ok, c_more, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed, c_p0,
+             c_lp, c_len, c_z, c_seed);
+        n_c = m_c;
+        issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
+        bool p_ok = false; // no row pending before the first step
+        uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_item = 0, p_chain = 0;
+        auto step = [&](u32x4 (&cb)[4], u32x4 (&mb)[4]) {
+          uint32_t m_item, m_lp;
+          uint64_t m_p0;
+          uint32_t m_r, m_len, m_z, m_nr, m_seed;
+          bool m_ok, m_more;
+          // succ() tracks the DYN counter index of the row it is given in c_c
+          // and leaves the successor's in m_c
+          const uint32_t cc = c_c;
+          c_c = n_c;
+          succ(n_ok, n_more, n_item, n_r, n_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, n_p0,
+               n_lp, n_len, n_z, n_seed);
+          c_c = cc;
+          issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, mb);
+          fix_row(c_lp, c_z, c_nr, c_r, cb);
+          uint32_t ch;
+          if constexpr (kLH) {
+            RPCCRC_CHAIN_ONLY(cb, ch);
+          } else {
+            RowMerge pm;
+            RPCCRC_CHAIN_MERGE(cb, ch, pm);
+            finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
+          }
+          publish();
+          p_ok = c_ok;
+          p_len = c_len;
+          p_z = c_z;
+          p_nr = c_nr;
+          p_r = c_r;
+          p_seed = c_seed;
+          p_c = c_c;
+          p_item = c_item;
+          p_chain = ch;
+          c_c = n_c;
+          c_ok = n_ok;
+          c_more = n_more;
+          c_seed = n_seed;
+          c_item = n_item;
+          c_r = n_r;
+          c_p0 = n_p0;
+          c_lp = n_lp;
+          c_len = n_len;
+          c_z = n_z;
+          c_nr = n_nr;
+          n_c = m_c;
+          n_ok = m_ok;
+          n_more = m_more;
+          n_seed = m_seed;
+          n_item = m_item;
+          n_r = m_r;
+          n_p0 = m_p0;
+          n_lp = m_lp;
+          n_len = m_len;
+          n_z = m_z;
+          n_nr = m_nr;
+        };
+        do {
+          step(bufA, bufC);
+          step(bufB, bufA);
+          step(bufC, bufB);
+        } while ((kS && steal) ? (n_more || c_more || p_ok) : p_ok);
+      } else if constexpr (DEPTH == 1 && kPipe) {
+        // Software pipeline over rows: one step issues row M's loads, runs row
+        // C's edge fix, transpose and chain, and merges row P (the row before C,
+        // whose chain the previous step computed).  C's chain and P's merge are
+        // independent and share one basic block, so the scheduler overlaps P's
+        // dependent merge lookups with C's chain.  Rows still finish in order
+        // (Horner across rows needs that).
+        u32x4 bufA[4], bufB[4];
+        issue(c_p0, c_lp, c_nr, c_r, c_ok, safe, bufA);
+        RPCCRC_ROWS_START();
+        bool p_ok = false; // no row pending before the first step
+        uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_item = 0, p_chain = 0;
+        auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
+          uint32_t m_item, m_lp;
+          uint64_t m_p0;
+          uint32_t m_r, m_len, m_z, m_nr, m_seed;
+          bool m_ok, m_more;
+          succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, c_p0,
+               c_lp, c_len, c_z, c_seed);
+          issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
+          fix_row(c_lp, c_z, c_nr, c_r, cb);
+          uint32_t ch;
+          if constexpr (kLH) {
+            RPCCRC_CHAIN_ONLY(cb, ch);
+          } else {
+            RowMerge pm;
+            RPCCRC_CHAIN_MERGE(cb, ch, pm);
+            finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
+          }
+          publish();
+          p_ok = c_ok;
+          p_len = c_len;
+          p_z = c_z;
+          p_nr = c_nr;
+          p_r = c_r;
+          p_seed = c_seed;
+          p_c = c_c;
+          p_item = c_item;
+          p_chain = ch;
+          c_c = m_c;
+          c_ok = m_ok;
+          c_more = m_more;
+          c_seed = m_seed;
+          c_item = m_item;
+          c_r = m_r;
+          c_p0 = m_p0;
+          c_lp = m_lp;
+          c_len = m_len;
+          c_z = m_z;
+          c_nr = m_nr;
+        };
+        do {
+          step(bufA, bufB);
+          step(bufB, bufA);
+        } while ((kS && steal) ? (c_more || p_ok) : p_ok);
+      } else if constexpr (DEPTH == 1) {
+        u32x4 bufA[4], bufB[4];
+        issue(c_p0, c_lp, c_nr, c_r, c_ok, safe, bufA);
+        RPCCRC_ROWS_START();
+        auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
+          uint32_t m_item, m_lp;
+          uint64_t m_p0;
+          uint32_t m_r, m_len, m_z, m_nr, m_seed;
+          bool m_ok, m_more;
+          succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, c_p0,
+               c_lp, c_len, c_z, c_seed);
+          issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
+          compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
+          publish();
+          c_c = m_c;
+          c_ok = m_ok;
+          c_more = m_more;
+          c_seed = m_seed;
+          c_item = m_item;
+          c_r = m_r;
+          c_p0 = m_p0;
+          c_lp = m_lp;
+          c_len = m_len;
+          c_z = m_z;
+          c_nr = m_nr;
+        };
+        do {
+          step(bufA, bufB);
+          step(bufB, bufA);
+        } while ((kS && steal) ? c_more : c_ok);
+      } else {
+        // DEPTH = 2: the next two rows' loads are in flight while one computes.
+        u32x4 bufA[4], bufB[4], bufC[4];
+        uint32_t n_item, n_lp;
+        uint64_t n_p0;
+        uint32_t n_r, n_len, n_z, n_nr, n_seed;
+        bool n_ok, n_more;
+        issue(c_p0, c_lp, c_nr, c_r, c_ok, safe, bufA);
+        RPCCRC_ROWS_START();
+        succ(true, true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed, c_p0, c_lp,
+             c_len, c_z, c_seed);
+        issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
+        auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) {
+          uint32_t m_item, m_lp;
+          uint64_t m_p0;
+          uint32_t m_r, m_len, m_z, m_nr, m_seed;
+          bool m_ok, m_more;
+          succ(n_ok, n_more, n_item, n_r, n_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, n_p0,
+               n_lp, n_len, n_z, n_seed);
+          issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
+          compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, c_item, cb);
+          c_ok = n_ok;
+          c_seed = n_seed;
+          n_seed = m_seed;
+          c_item = n_item;
+          c_r = n_r;
+          c_lp = n_lp;
+          c_len = n_len;
+          c_z = n_z;
+          c_nr = n_nr;
+          n_ok = m_ok;
+          n_item = m_item;
+          n_r = m_r;
+          n_p0 = m_p0;
+          n_lp = m_lp;
+          n_len = m_len;
+          n_z = m_z;
+          n_nr = m_nr;
+        };
+        do {
+          step(bufA, bufC);
+          step(bufB, bufA);
+          step(bufC, bufB);
+        } while (c_ok);
       }
     };
-    if constexpr (DEPTH == 1 && kPipe && kRaggedAhead2) {
-      // The pipeline below with loads two rows ahead: one step issues row M's
-      // loads while row N's (the row after C) are in flight, chains row C and
-      // merges row P.  A wave then keeps a row of loads in flight while it
-      // computes, also across item switches (C2's memory-only variant runs
-      // 5.79 ms against 6.33 for the product with one row ahead).
-      u32x4 bufA[4], bufB[4], bufC[4];
-      issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      RPCCRC_ROWS_START();
-      uint32_t n_item, n_lp, n_r, n_len, n_z, n_nr, n_seed, n_c;
-      uint64_t n_p0;
-      bool n_ok, n_more;
-      succ(c_ok, c_more, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed, c_p0,
-           c_lp, c_len, c_z, c_seed);
-      n_c = m_c;
-      issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
-      bool p_ok = false; // no row pending before the first step
-      uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_item = 0, p_chain = 0;
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&mb)[4]) {
-        uint32_t m_item, m_lp;
-        uint64_t m_p0;
-        uint32_t m_r, m_len, m_z, m_nr, m_seed;
-        bool m_ok, m_more;
-        // succ() tracks the DYN counter index of the row it is given in c_c
-        // and leaves the successor's in m_c
-        const uint32_t cc = c_c;
-        c_c = n_c;
-        succ(n_ok, n_more, n_item, n_r, n_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, n_p0,
-             n_lp, n_len, n_z, n_seed);
-        c_c = cc;
-        issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, mb);
-        fix_row(c_lp, c_z, c_nr, c_r, cb);
-        uint32_t ch;
-        if constexpr (kLH) {
-          RPCCRC_CHAIN_ONLY(cb, ch);
-        } else {
-          RowMerge pm;
-          RPCCRC_CHAIN_MERGE(cb, ch, pm);
-          finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
-        }
-        publish();
-        p_ok = c_ok;
-        p_len = c_len;
-        p_z = c_z;
-        p_nr = c_nr;
-        p_r = c_r;
-        p_seed = c_seed;
-        p_c = c_c;
-        p_item = c_item;
-        p_chain = ch;
-        c_c = n_c;
-        c_ok = n_ok;
-        c_more = n_more;
-        c_seed = n_seed;
-        c_item = n_item;
-        c_r = n_r;
-        c_p0 = n_p0;
-        c_lp = n_lp;
-        c_len = n_len;
-        c_z = n_z;
-        c_nr = n_nr;
-        n_c = m_c;
-        n_ok = m_ok;
-        n_more = m_more;
-        n_seed = m_seed;
-        n_item = m_item;
-        n_r = m_r;
-        n_p0 = m_p0;
-        n_lp = m_lp;
-        n_len = m_len;
-        n_z = m_z;
-        n_nr = m_nr;
-      };
-      do {
-        step(bufA, bufC);
-        step(bufB, bufA);
-        step(bufC, bufB);
-      } while (steal ? (n_more || c_more || p_ok) : p_ok);
-    } else if constexpr (DEPTH == 1 && kPipe) {
-      // Software pipeline over rows: one step issues row M's loads, runs row
-      // C's edge fix, transpose and chain, and merges row P (the row before C,
-      // whose chain the previous step computed).  C's chain and P's merge are
-      // independent and share one basic block, so the scheduler overlaps P's
-      // dependent merge lookups with C's chain.  Rows still finish in order
-      // (Horner across rows needs that).
-      u32x4 bufA[4], bufB[4];
-      issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      RPCCRC_ROWS_START();
-      bool p_ok = false; // no row pending before the first step
-      uint32_t p_len = 0, p_z = 0, p_nr = 1, p_r = 0, p_seed = 0, p_c = 0, p_item = 0, p_chain = 0;
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
-        uint32_t m_item, m_lp;
-        uint64_t m_p0;
-        uint32_t m_r, m_len, m_z, m_nr, m_seed;
-        bool m_ok, m_more;
-        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, c_p0,
-             c_lp, c_len, c_z, c_seed);
-        issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
-        fix_row(c_lp, c_z, c_nr, c_r, cb);
-        uint32_t ch;
-        if constexpr (kLH) {
-          RPCCRC_CHAIN_ONLY(cb, ch);
-        } else {
-          RowMerge pm;
-          RPCCRC_CHAIN_MERGE(cb, ch, pm);
-          finish(p_ok, p_len, p_z, p_nr, p_r, p_seed, p_c, p_item, pm);
-        }
-        publish();
-        p_ok = c_ok;
-        p_len = c_len;
-        p_z = c_z;
-        p_nr = c_nr;
-        p_r = c_r;
-        p_seed = c_seed;
-        p_c = c_c;
-        p_item = c_item;
-        p_chain = ch;
-        c_c = m_c;
-        c_ok = m_ok;
-        c_more = m_more;
-        c_seed = m_seed;
-        c_item = m_item;
-        c_r = m_r;
-        c_p0 = m_p0;
-        c_lp = m_lp;
-        c_len = m_len;
-        c_z = m_z;
-        c_nr = m_nr;
-      };
-      do {
-        step(bufA, bufB);
-        step(bufB, bufA);
-      } while (steal ? (c_more || p_ok) : p_ok);
-    } else if constexpr (DEPTH == 1) {
-      u32x4 bufA[4], bufB[4];
-      issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      RPCCRC_ROWS_START();
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
-        uint32_t m_item, m_lp;
-        uint64_t m_p0;
-        uint32_t m_r, m_len, m_z, m_nr, m_seed;
-        bool m_ok, m_more;
-        succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, c_p0,
-             c_lp, c_len, c_z, c_seed);
-        issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
-        publish();
-        c_c = m_c;
-        c_ok = m_ok;
-        c_more = m_more;
-        c_seed = m_seed;
-        c_item = m_item;
-        c_r = m_r;
-        c_p0 = m_p0;
-        c_lp = m_lp;
-        c_len = m_len;
-        c_z = m_z;
-        c_nr = m_nr;
-      };
-      do {
-        step(bufA, bufB);
-        step(bufB, bufA);
-      } while (steal ? c_more : c_ok);
-    } else {
-      // DEPTH = 2: the next two rows' loads are in flight while one computes.
-      u32x4 bufA[4], bufB[4], bufC[4];
-      uint32_t n_item, n_lp;
-      uint64_t n_p0;
-      uint32_t n_r, n_len, n_z, n_nr, n_seed;
-      bool n_ok, n_more;
-      issue(c_p0, c_lp, c_nr, c_r, true, safe, bufA);
-      RPCCRC_ROWS_START();
-      succ(true, true, c_item, c_r, c_nr, n_item, n_r, n_ok, n_more, n_p0, n_lp, n_len, n_z, n_nr, n_seed, c_p0, c_lp,
-           c_len, c_z, c_seed);
-      issue(n_p0, n_lp, n_nr, n_r, n_ok, safe, bufB);
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&fb)[4]) {
-        uint32_t m_item, m_lp;
-        uint64_t m_p0;
-        uint32_t m_r, m_len, m_z, m_nr, m_seed;
-        bool m_ok, m_more;
-        succ(n_ok, n_more, n_item, n_r, n_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, n_p0,
-             n_lp, n_len, n_z, n_seed);
-        issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, fb);
-        compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, 0, c_item, cb);
-        c_ok = n_ok;
-        c_seed = n_seed;
-        n_seed = m_seed;
-        c_item = n_item;
-        c_r = n_r;
-        c_lp = n_lp;
-        c_len = n_len;
-        c_z = n_z;
-        c_nr = n_nr;
-        n_ok = m_ok;
-        n_item = m_item;
-        n_r = m_r;
-        n_p0 = m_p0;
-        n_lp = m_lp;
-        n_len = m_len;
-        n_z = m_z;
-        n_nr = m_nr;
-      };
-      do {
-        step(bufA, bufC);
-        step(bufB, bufA);
-        step(bufC, bufB);
-      } while (c_ok);
-    }
+    rows_phase(std::integral_constant<int, 1>{});
+    if constexpr (STEAL)
+      if (steal) rows_phase(std::integral_constant<int, 2>{});
     } // (!kSB)
     publish();
     flush();
@@ -2160,57 +2193,91 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t g = first_task;
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
-      u32x4 bufA[4], bufB[4];
-      QuadMeta c_qm = issue(g, true, safe, bufA);
-      if constexpr (kEarly) RPCCRC_ROWS_BEGIN();
+      // Stealing launches in two phases, as QB = 1 (the loop without the pool
+      // protocol, then the one with it).
       uint32_t pend = 0;
-      if constexpr (DYN) pend = dyn_grab();
-      uint32_t c_c = first_c;
-      bool c_ok = true;   // the group being computed next is real
-      bool c_more = true; // stealing: the wave may still get groups (a group past the end is skipped)
-      // One exit, at the bottom (see QB = 1): a mid-body break made the
-      // compiler drain vmcnt before the next group's loads on every step
-      // (ISA: s_waitcnt vmcnt(0) ahead of the offset of the 4th quarter load).
-      // Steps past the wave's last group load nothing and store nothing.
-      auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
-        uint32_t ng, n_c = 0;
-        bool ok, more = false;
-        if constexpr (STEAL) {
-          ng = ngroups;
-          if (c_more) {
-            n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-            claim_if_first(n_c);
-            ng = dyn_map(n_c, more);
-            if (more) pend = dyn_grab();
-          }
-          // uniform again after the lane-0 grab (else the compiler carried
-          // `more` as a lane mask and the group index went to VGPRs)
+      const uint32_t p1_lim = steal ? (steal_s - kStealAhead) * kRound : 0xFFFFFFFFu;
+      const uint32_t g0 = g;
+      auto rows_phase4 = [&](auto ph) {
+        constexpr int kPh = decltype(ph)::value;
+        constexpr bool kS = STEAL && kPh == 2;
+        u32x4 bufA[4], bufB[4];
+        uint32_t c_c = first_c;
+        bool c_ok = true;   // the group being computed next is real
+        bool c_more = true; // stealing: the wave may still get groups (a group past the end is skipped)
+        QuadMeta c_qm;
+        if constexpr (kPh == 2) { // from the task phase 1 grabbed and left
+          c_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+          claim_if_first(c_c);
+          bool more = false;
+          const uint32_t t0 = dyn_map(c_c, more);
           more = __builtin_amdgcn_readfirstlane((int)more) != 0;
-          ok = more && ng < ngroups;
+          c_more = more;
+          c_ok = more && t0 < ngroups;
+          g = c_ok ? t0 : g0;
+          if (more) pend = dyn_grab();
+          c_qm = issue(g, c_ok, safe, bufA);
         } else {
-          if constexpr (DYN) {
-            n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
-            ng = dyn_task(n_c);
-          } else {
-            ng = next_task(g);
-          }
-          ok = c_ok && ng < ngroups;
-          if constexpr (DYN)
-            if (ok) pend = dyn_grab();
+          c_qm = issue(g, true, safe, bufA);
+          if constexpr (kEarly) RPCCRC_ROWS_BEGIN();
+          if constexpr (DYN) pend = dyn_grab();
         }
-        const QuadMeta n_qm = issue(ok ? ng : g, ok, safe, nb);
-        compute(c_qm, c_ok, c_c, g, cb);
-        publish();
-        c_qm = n_qm;
-        g = ok ? ng : g;
-        c_c = n_c;
-        c_ok = ok;
-        c_more = more;
+        // One exit, at the bottom (see QB = 1): a mid-body break made the
+        // compiler drain vmcnt before the next group's loads on every step
+        // (ISA: s_waitcnt vmcnt(0) ahead of the offset of the 4th quarter load).
+        // Steps past the wave's last group load nothing and store nothing.
+        auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
+          uint32_t ng, n_c = 0;
+          bool ok, more = false;
+          if constexpr (kS) {
+            ng = ngroups;
+            if (c_more) {
+              n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+              claim_if_first(n_c);
+              ng = dyn_map(n_c, more);
+              if (more) pend = dyn_grab();
+            }
+            // uniform again after the lane-0 grab (else the compiler carried
+            // `more` as a lane mask and the group index went to VGPRs)
+            more = __builtin_amdgcn_readfirstlane((int)more) != 0;
+            ok = more && ng < ngroups;
+          } else {
+            if constexpr (DYN) {
+              n_c = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend);
+              ng = dyn_task(n_c);
+              if constexpr (STEAL) if (n_c >= p1_lim) ng = ngroups; // phase 1 ends (as QB = 1)
+            } else {
+              ng = next_task(g);
+            }
+            ok = c_ok && ng < ngroups;
+            // the next group as an SGPR before the lane-0 grab: the compiler
+            // otherwise sank its select into the grab's exec-masked region
+            // and carried the group index in a VGPR (the loop's SALU work
+            // went to the VALU, ISA)
+            uint32_t gn = ok ? ng : g;
+            __asm__ volatile("" : "+s"(gn));
+            ng = gn;
+            if constexpr (DYN)
+              if (ok) pend = dyn_grab();
+          }
+          if constexpr (kS) ng = ok ? ng : g;
+          const QuadMeta n_qm = issue(ng, ok, safe, nb);
+          compute(c_qm, c_ok, c_c, g, cb);
+          publish();
+          c_qm = n_qm;
+          g = ng;
+          c_c = n_c;
+          c_ok = ok;
+          c_more = more;
+        };
+        do {
+          step(bufA, bufB);
+          step(bufB, bufA);
+        } while ((kS && steal) ? c_more : c_ok);
       };
-      do {
-        step(bufA, bufB);
-        step(bufB, bufA);
-      } while (steal ? c_more : c_ok);
+      rows_phase4(std::integral_constant<int, 1>{});
+      if constexpr (STEAL)
+        if (steal) rows_phase4(std::integral_constant<int, 2>{});
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;

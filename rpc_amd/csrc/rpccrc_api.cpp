@@ -617,12 +617,15 @@ struct StealLease {
   hipEvent_t done_event() const { return steal_ext_event() && slot ? slot->ev : nullptr; }
 };
 
-// Tail stealing for ragged rows passes (off: C2 +0.7 % in round 2, +2.3 % in
-// round 3 with a 15 % or 5 % pool, profiles/r03e/c2_ragged_steal_ab.txt).
+// Tail stealing for ragged rows passes: on since round 5's two-phase loop
+// (crc32_rows.h; a 3 % pool, crc32_kernels.hip steal_frac): C2 -0.5 to -0.9 %
+// against no pool, rotated (profiles/r05z).  Before it, the pool protocol in
+// the one loop made every row dearer and stealing cost C2 +0.7 % (round 2),
+// +2.3 % (round 3), +1.8 % (round 5, r05w).  RPCCRC_RAGGED_STEAL=0 turns it off.
 bool ragged_steal() {
   static const bool v = [] {
     const char *e = getenv("RPCCRC_RAGGED_STEAL");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -769,9 +772,9 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     sl.s = s;
     if (span_rows)
       if (const int rc = ssl.get(c, span_rows, 1, s)) return rc;
-    a.test_giveup = take_test_giveup(); // (the plain rows pass does not steal)
+    a.test_giveup = take_test_giveup(); // (the route's chunk pass; the plain rows pass takes its own below)
   }
-  StealLease rsl; // RPCCRC_RAGGED_STEAL=1: the plain rows pass deals its tail from a steal counter too
+  StealLease rsl; // the plain rows pass deals its tail from a steal counter too (RPCCRC_RAGGED_STEAL=0: not)
   if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
   } else if (!route_all) {
@@ -779,8 +782,11 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
       if (const int rc = rsl.get(c, n, 1, s)) return rc;
       a.steal = rsl.p;
     }
+    const uint32_t route_giveup = a.test_giveup;
+    a.test_giveup = a.steal ? take_test_giveup() : 0u;
     RPCCRC_TRY(launch_rows(a, 1, nt, mb, s, rsl.done_event(), &rsl.recorded));
     a.steal = nullptr;
+    a.test_giveup = route_giveup;
   }
   if (route) {
     StealArgs span;

@@ -134,12 +134,13 @@ def timeline(w, a):
     if ragged:  # the C2 path: ragged QB = 1, DYN (static rounds, as the product)
         lib.probe_rows_ragged_times.restype = ctypes.c_int
         lib.probe_rows_ragged_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
-                                                ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+                                                ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int]
 
     def f():
         if ragged:
             rc = lib.probe_rows_ragged_times(w.base.data_ptr(), w.offs.data_ptr(), w.lens.data_ptr(), w.n,
-                                             out.data_ptr(), 256, s.cuda_stream, times.data_ptr())
+                                             out.data_ptr(), 256, s.cuda_stream, times.data_ptr(), int(a.steal))
         else:
             rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1,
                                       512 | (1024 if a.dyn or a.steal else 0) | (4096 if a.steal else 0), 1, 256,

@@ -144,7 +144,7 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_ragged(const ui
 extern "C" __attribute__((visibility("default"))) int probe_rows_ragged_times(const uint8_t *d_base, const uint64_t *d_offs,
                                                                                const uint32_t *d_lens, uint64_t n,
                                                                                uint32_t *d_out, int blocks, void *stream,
-                                                                               uint64_t *d_times) {
+                                                                               uint64_t *d_times, int steal) {
   if (ensure_tables()) return -12;
   ItemsArgs a;
   a.base = d_base;
@@ -159,8 +159,21 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_ragged_times(co
   a.out = d_out;
   a.gshift = 0;
   a.round_out = reinterpret_cast<uint32_t *>(d_times);
-  hipLaunchKernelGGL((crc32_rows_kernel<1, true, true, kRowsAblTimes, 1, true>), dim3(blocks), dim3(1024), 0,
-                     static_cast<hipStream_t>(stream), a);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (steal) { // the product's pool sizing (launch_rows): 8 %, at most 48 pool rounds per workgroup
+    static uint32_t *ctr = nullptr;
+    if (!ctr && hipMalloc(&ctr, 64) != hipSuccess) return -12;
+    if (hipMemsetAsync(ctr, 0, 64, s) != hipSuccess) return -5;
+    const uint64_t rounds = (n + kDynRound - 1) / kDynRound;
+    uint64_t st = (uint64_t)((double)rounds * 0.92) / (uint64_t)blocks;
+    if (rounds / blocks > st + 48) st = rounds / blocks - 48;
+    a.steal = ctr;
+    a.steal_s = (uint32_t)st;
+    hipLaunchKernelGGL((crc32_rows_kernel<1, true, true, kRowsAblTimes, 1, true, true>), dim3(blocks), dim3(1024), 0,
+                       s, a);
+  } else {
+    hipLaunchKernelGGL((crc32_rows_kernel<1, true, true, kRowsAblTimes, 1, true>), dim3(blocks), dim3(1024), 0, s, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
