@@ -690,6 +690,10 @@ constexpr bool kRaggedAhead2 = RPCCRC_RAGGED_AHEAD2 != 0;
 #define RPCCRC_EARLY_ROW 1
 #endif
 constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
+#ifndef RPCCRC_QB4_TWO_PHASE
+#define RPCCRC_QB4_TWO_PHASE 0
+#endif
+constexpr bool kQb4TwoPhase = RPCCRC_QB4_TWO_PHASE != 0;
 #ifndef RPCCRC_STEAL_EXIT_ACQREL
 #define RPCCRC_STEAL_EXIT_ACQREL 0
 #endif
@@ -2193,14 +2197,17 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t g = first_task;
     const uint64_t safe = (uint64_t)(uintptr_t)quarter(g, 0).p0 & ~(uint64_t)15;
     if constexpr (DEPTH == 1) {
-      // Stealing launches in two phases, as QB = 1 (the loop without the pool
-      // protocol, then the one with it).
+      // Stealing launches in two phases as QB = 1 (the loop without the pool
+      // protocol, then the one with it) only with RPCCRC_QB4_TWO_PHASE=1: C1's
+      // launches are 32 rounds a workgroup, and the pipeline drain and refill
+      // at the phase switch cost more than the cheaper static loop saves (C1
+      // +0.5 %, profiles/r05zc).  Phase 3: one loop with the protocol.
       uint32_t pend = 0;
       const uint32_t p1_lim = steal ? (steal_s - kStealAhead) * kRound : 0xFFFFFFFFu;
       const uint32_t g0 = g;
       auto rows_phase4 = [&](auto ph) {
         constexpr int kPh = decltype(ph)::value;
-        constexpr bool kS = STEAL && kPh == 2;
+        constexpr bool kS = STEAL && kPh >= 2;
         u32x4 bufA[4], bufB[4];
         uint32_t c_c = first_c;
         bool c_ok = true;   // the group being computed next is real
@@ -2275,9 +2282,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           step(bufB, bufA);
         } while ((kS && steal) ? c_more : c_ok);
       };
-      rows_phase4(std::integral_constant<int, 1>{});
-      if constexpr (STEAL)
-        if (steal) rows_phase4(std::integral_constant<int, 2>{});
+      if constexpr (STEAL && !kQb4TwoPhase) {
+        rows_phase4(std::integral_constant<int, 3>{});
+      } else {
+        rows_phase4(std::integral_constant<int, 1>{});
+        if constexpr (STEAL)
+          if (steal) rows_phase4(std::integral_constant<int, 2>{});
+      }
     } else {
       u32x4 bufA[4], bufB[4], bufC[4];
       QuadMeta c_qm = issue(g, true, safe, bufA), n_qm;
