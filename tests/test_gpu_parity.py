@@ -394,6 +394,30 @@ def test_device_batch_split_workgroup_dynamic(misalign):
         rpc_amd.set_ragged_path("auto")
 
 
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 33, 4095, 65536 + 5])
+def test_split_small_body_kernel_counts(n):
+    """The split path's small-body kernel (crc32_small.h): a wave walks whole
+    iterations of 16 bodies of its list range, so counts that are not multiples
+    of 16, lists shorter than one wave's share and lists much shorter than the
+    batch (the grid is sized for the batch) all have to come out exact.  Bodies
+    of 0..1024 B at every 16-B phase (those whose end pad pushes them past 1 KiB
+    go to the other list), a few large ones mixed in; unordered offsets."""
+    rng = np.random.default_rng(4000 + n)
+    lens = rng.integers(0, 1025, n).astype(np.uint32)
+    lens[::11] = 0
+    big = rng.random(n) < 0.1
+    lens[big] = rng.integers(1025, 20000, int(big.sum()))
+    gaps = rng.integers(0, 16, n).astype(np.uint64)
+    offs = (np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])]) + gaps[0]).astype(np.uint64)
+    perm = rng.permutation(n)
+    host = oracle.splitmix_bytes(int(offs[-1]) + int(lens[-1]) + 32, 4000 + n)
+    rpc_amd.set_ragged_path("split")
+    try:
+        _ragged_check(host, offs[perm].copy(), lens[perm].copy())
+    finally:
+        rpc_amd.set_ragged_path("auto")
+
+
 def test_ragged_path_option():
     with pytest.raises(rpc_amd.RpcCrcError):
         rpc_amd.set_ragged_path(7)

@@ -140,7 +140,8 @@ def timeline(w, a):
     def f():
         if ragged:
             rc = lib.probe_rows_ragged_times(w.base.data_ptr(), w.offs.data_ptr(), w.lens.data_ptr(), w.n,
-                                             out.data_ptr(), 256, s.cuda_stream, times.data_ptr(), int(a.steal))
+                                             out.data_ptr(), 256, s.cuda_stream, times.data_ptr(),
+                                             a.steal_pct if a.steal else 0)
         else:
             rc = lib.probe_rows_times(w.base.data_ptr(), w.n, w.L, w.L, out.data_ptr(), qb, 1, 1,
                                       512 | (1024 if a.dyn or a.steal else 0) | (4096 if a.steal else 0), 1, 256,
@@ -414,6 +415,7 @@ def main():
     ap.add_argument("--gshift", type=int, default=0, help="timeline: group-dealing shift of the rows kernel")
     ap.add_argument("--dyn", action="store_true", help="timeline: workgroup-dynamic dealing (DYN)")
     ap.add_argument("--steal", action="store_true", help="timeline: DYN with the product's tail stealing")
+    ap.add_argument("--steal-pct", type=int, default=3, help="timeline, ragged: pool percent with --steal")
     ap.add_argument("--save", default="", help="timeline: save per-wave times to <save>_rep<k>.npy")
     a = ap.parse_args()
     torch.cuda.set_device(0)

@@ -160,12 +160,12 @@ extern "C" __attribute__((visibility("default"))) int probe_rows_ragged_times(co
   a.gshift = 0;
   a.round_out = reinterpret_cast<uint32_t *>(d_times);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (steal) { // the product's pool sizing (launch_rows): 8 %, at most 48 pool rounds per workgroup
+  if (steal) { // the product's pool sizing (launch_rows): steal % of the rounds, at most 48 per workgroup
     static uint32_t *ctr = nullptr;
     if (!ctr && hipMalloc(&ctr, 64) != hipSuccess) return -12;
     if (hipMemsetAsync(ctr, 0, 64, s) != hipSuccess) return -5;
     const uint64_t rounds = (n + kDynRound - 1) / kDynRound;
-    uint64_t st = (uint64_t)((double)rounds * 0.92) / (uint64_t)blocks;
+    uint64_t st = (uint64_t)((double)rounds * (1.0 - steal / 100.0)) / (uint64_t)blocks;
     if (rounds / blocks > st + 48) st = rounds / blocks - 48;
     a.steal = ctr;
     a.steal_s = (uint32_t)st;
