@@ -690,6 +690,10 @@ constexpr bool kRaggedAhead2 = RPCCRC_RAGGED_AHEAD2 != 0;
 #define RPCCRC_EARLY_ROW 1
 #endif
 constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
+#ifndef RPCCRC_TWO_PHASE
+#define RPCCRC_TWO_PHASE 1
+#endif
+constexpr bool kTwoPhase = RPCCRC_TWO_PHASE != 0;
 #ifndef RPCCRC_QB4_TWO_PHASE
 #define RPCCRC_QB4_TWO_PHASE 0
 #endif
@@ -1571,8 +1575,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     uint32_t pend = 0; // DYN: lane 0 holds the counter index grabbed a task ahead
     const uint32_t p1_lim = steal ? (steal_s - kStealAhead) * kRound : 0xFFFFFFFFu;
     auto rows_phase = [&](auto ph) {
-      constexpr int kPh = decltype(ph)::value; // 1: plain loop (all of a launch without a pool), 2: pool phase
-      constexpr bool kS = STEAL && kPh == 2;   // the pool protocol compiled in
+      // 1: plain loop (all of a launch without a pool), 2: pool phase, 3: one
+      // loop with the protocol (RPCCRC_TWO_PHASE=0, rounds 2-4)
+      constexpr int kPh = decltype(ph)::value;
+      constexpr bool kS = STEAL && kPh >= 2; // the pool protocol compiled in
       uint32_t c_item = first_task;
       uint32_t c_c = first_c, m_c = 0; // DYN: counter index of the current / successor item
       // more: the wave may still get work (stealing: a task past n inside a
@@ -1962,9 +1968,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         } while (c_ok);
       }
     };
-    rows_phase(std::integral_constant<int, 1>{});
-    if constexpr (STEAL)
-      if (steal) rows_phase(std::integral_constant<int, 2>{});
+    if constexpr (STEAL && !kTwoPhase) {
+      rows_phase(std::integral_constant<int, 3>{});
+    } else {
+      rows_phase(std::integral_constant<int, 1>{});
+      if constexpr (STEAL)
+        if (steal) rows_phase(std::integral_constant<int, 2>{});
+    }
     } // (!kSB)
     publish();
     flush();
