@@ -282,6 +282,18 @@ RPCCRC_API int rpc_crc32_device_status(void);
  * doubt: outputs of the launch that failed are not repaired. */
 RPCCRC_API int rpc_crc32_device_clear_status(void);
 
+/* Stops the resident drop-in service kernel (the one that answers rpc_crc32 /
+ * rpc_crc32_verify calls of <= 1 KiB without a launch) on every
+ * device this process has used, and waits (up to 200 ms each) until it has left.
+ * A device-wide synchronise (hipDeviceSynchronize, torch.cuda.synchronize())
+ * otherwise waits for the service: up to ~2 ms after the last drop-in call
+ * (INTEGRATION.md 5).  The next drop-in call starts it again.  Call it with no
+ * drop-in call in flight: one racing it waits for its answer (up to 2 s) and then
+ * launches a kernel instead.  Returns RPCCRC_OK, or RPCCRC_EIO if an instance did
+ * not leave in time (it was still queued behind other work; it then runs and
+ * serves calls as usual).  Not part of crc.h; the reference has no counterpart. */
+RPCCRC_API int rpc_crc32_service_stop(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -297,6 +297,12 @@ def device_clear_status() -> int:
     return int(_lib.rpc_crc32_device_clear_status())
 
 
+def service_stop() -> int:
+    """Stops the resident drop-in service (the next drop-in call restarts it), so a
+    device-wide synchronize does not wait for it; 0, or -5 if it did not leave in time."""
+    return int(_lib.rpc_crc32_service_stop())
+
+
 def device_info() -> str:
     buf = ctypes.create_string_buffer(256)
     check(_lib.rpc_crc32_device_info(buf, 256), "rpc_crc32_device_info")

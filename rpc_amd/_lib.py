@@ -80,6 +80,7 @@ rpc_crc32_strerror = _sig("rpc_crc32_strerror", ctypes.c_char_p, _i32)
 rpc_crc32_device_info = _sig("rpc_crc32_device_info", _i32, ctypes.c_char_p, _sz)
 rpc_crc32_device_status = _sig("rpc_crc32_device_status", _i32)
 rpc_crc32_device_clear_status = _sig("rpc_crc32_device_clear_status", _i32)
+rpc_crc32_service_stop = _sig("rpc_crc32_service_stop", _i32)
 
 #: Every symbol include/rpccrc.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -109,6 +110,7 @@ EXPORTS = (
     "rpc_crc32_device_info",
     "rpc_crc32_device_status",
     "rpc_crc32_device_clear_status",
+    "rpc_crc32_service_stop",
 )
 
 

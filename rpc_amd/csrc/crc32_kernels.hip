@@ -250,6 +250,13 @@ static double steal_frac(int QB = 1, bool ragged = false) {
   static const double fr = env_frac("RPCCRC_STEAL_FRAC_RAGGED", 0.03);
   return QB == 4 ? f4 : ragged ? fr : f1;
 }
+// Device-counted launches (the big-body route's chunk and span passes, sized in
+// the kernel) keep the round-4 pool of 8 %: lifted-cap frames verify 543-545 us
+// with it against 554-567 with 5 % (rotated, one box, profiles/r05fl2).
+static double steal_frac_dev() {
+  static const double f = env_frac("RPCCRC_STEAL_FRAC_DEV", 0.08);
+  return f;
+}
 // ... but at most this many pool rounds per workgroup: the pool has to absorb
 // the workgroups' spread in finishing time, not a share of an ever larger
 // batch, and every pool round costs a device-scope claim.  C3 (8M x 4 KiB,
@@ -309,7 +316,7 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
   // rounds go to the device-counter pool, the rest stay static per workgroup.
   ItemsArgs k = a;
   k.steal_s = 0;
-  k.steal_permille = (uint32_t)(steal_frac(QB, ragged) * 1000.0 + 0.5);
+  k.steal_permille = (uint32_t)(steal_frac_dev() * 1000.0 + 0.5); // (device-counted launches only)
   k.steal_max_wg = steal_max_per_wg();
   if (dyn && a.steal != nullptr && a.n_dev == nullptr) {
     const uint64_t rounds = (n_tasks + round - 1) / round;

@@ -1970,10 +1970,18 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     if constexpr (STEAL && !kTwoPhase) {
       rows_phase(std::integral_constant<int, 3>{});
+    } else if constexpr (STEAL) {
+      // Device-counted launches (the big-body route's chunk and span passes)
+      // keep one loop, as in rounds 2-4: lifted-cap frames ran 1-2 % slower with
+      // two phases (profiles/r05fl2).
+      if (a.steal_s == kStealOnDevice) {
+        rows_phase(std::integral_constant<int, 3>{});
+      } else {
+        rows_phase(std::integral_constant<int, 1>{});
+        if (steal) rows_phase(std::integral_constant<int, 2>{});
+      }
     } else {
       rows_phase(std::integral_constant<int, 1>{});
-      if constexpr (STEAL)
-        if (steal) rows_phase(std::integral_constant<int, 2>{});
     }
     } // (!kSB)
     publish();

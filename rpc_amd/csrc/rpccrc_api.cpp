@@ -1145,6 +1145,25 @@ bool svc_running(const Service &v) {
          v.launched.load(std::memory_order_acquire);
 }
 
+// rpc_crc32_service_stop: the running instances leave now; the stop word is
+// cleared again so the next drop-in call's instance serves as usual.
+int svc_stop_all() {
+  std::lock_guard<std::mutex> g(g_services_mu);
+  int rc = RPCCRC_OK;
+  for (Service *v : g_services) {
+    std::lock_guard<std::mutex> lg(v->launch_mu); // no instance starts meanwhile
+    if (!svc_running(*v)) continue;
+    volatile uint32_t *ctl = v->sh->ctl;
+    ctl[kSvcStop] = 1u;
+    const uint64_t t0 = mono_ns();
+    while (svc_running(*v) && mono_ns() - t0 < 200000000ull) {
+    }
+    if (svc_running(*v)) rc = RPCCRC_EIO;
+    ctl[kSvcStop] = 0u;
+  }
+  return rc;
+}
+
 // Launches an instance unless one is running (the new one queues behind a
 // leaving one on the service stream).
 bool svc_ensure(DeviceCtx &c, Service &v) {
@@ -1615,6 +1634,8 @@ int rpc_crc32_device_status(void) {
   DeviceCtx *c = nullptr;
   return get_async_ctx(&c);
 }
+
+int rpc_crc32_service_stop(void) { return svc_stop_all(); }
 
 int rpc_crc32_device_clear_status(void) {
   DeviceCtx *c = nullptr;

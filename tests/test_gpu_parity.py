@@ -1053,3 +1053,23 @@ for i, b in enumerate(bodies * 3):
     # the three muted (inline) calls waited out the 20 ms and fell back
     slow = [int(r[1]) for r in rows if float(r[4]) >= 19.0]
     assert len(slow) == 3, p.stdout
+
+
+def test_drop_in_service_stop():
+    """rpc_crc32_service_stop (a device-wide synchronize waits for the
+    resident service): after a burst of drop-in calls the service leaves on request,
+    a torch.cuda.synchronize() then has nothing of it to wait for, and the next
+    drop-in calls restart it and answer with the oracle CRC.  Stopping with no
+    service running is a no-op."""
+    import time
+    bodies = [oracle.splitmix_bytes(k, 0x5709 + k) for k in (9, 68, 116, 117, 1024)]
+    for _ in range(3):
+        for b in bodies:
+            assert rpc_amd.rpc_crc32(b) == oracle.crc32(b)
+        assert rpc_amd.service_stop() == 0
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        sync_ms = (time.perf_counter() - t0) * 1e3
+        assert sync_ms < 50.0, sync_ms  # (the service's own life cap is 20 ms)
+    assert rpc_amd.service_stop() == 0  # nothing running
+    assert rpc_amd.rpc_crc32(b"123456789") == 0xCBF43926
