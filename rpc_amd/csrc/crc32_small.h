@@ -52,8 +52,19 @@ __global__ void __launch_bounds__(1024, 4) crc32_small_kernel(ItemsArgs a) {
   using namespace rows;
   using namespace small;
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytesV2 / 4];
+  // Edge masks of a quarter's two edge pieces, one 16-B row per case: [f] keeps
+  // bytes >= f of the piece holding the body's first byte, [16 + z] bytes below
+  // 16 - z of the window's last piece (its z pad).  Four scalar masks per fix
+  // cost ~16 SALU; a row has up to eight fixes, and one scalar unit serves the
+  // CU's 16 waves (the kernel was SALU-bound: 310 SALU per row, profiles/r05u).
+  __shared__ __attribute__((aligned(16))) uint32_t s_mask[2 * 16 * 4];
+  static_assert(sizeof(s_lds) + sizeof(s_mask) <= kRowsLdsMax, "leave a CU room for the drop-in service");
   const uint64_t n = a.n_dev ? ld_const(a.n_dev, 0) : a.n_items;
   if (n == 0) return; // (block-uniform: before the image copy)
+  if (threadIdx.x < 128u) {
+    const uint32_t t = threadIdx.x, k = (t >> 2) & 15u, d = t & 3u;
+    s_mask[t] = (t < 64u) ? keep_front_dword(k, d) : keep_end_dword(16u - k, d);
+  }
   copy_lds_image<kLdsBytesV2>(a.lds_image, s_lds);
   __syncthreads();
   const uint8_t *lds = reinterpret_cast<const uint8_t *>(s_lds);
@@ -133,11 +144,21 @@ __global__ void __launch_bounds__(1024, 4) crc32_small_kernel(ItemsArgs a) {
   // Row k's four CRCs into lanes 4k .. 4k + 3 of outv.
   auto compute = [&](const Meta &m, uint32_t k, u32x4 (&buf)[4], uint32_t &outv) {
     uint32_t lz[4], zany = 0, zl = 0, sl = 0;
+    const uint32_t e_end = (lane == lane_of_piece(63u)) ? 0u : 0xFFFFFFFFu; // the window's last piece
 #pragma unroll
     for (uint32_t b = 0; b < 4; ++b) {
       lz[b] = __builtin_amdgcn_readlane(m.len, 4u * k + b);
       const uint32_t len = lz[b] >> 4, z = lz[b] & 15u;
-      if (len != 0u) fix_quarter<false>(buf[b], lane, kQuarter - len - z, z);
+      // both edge fixes, unconditionally (rows::fix_quarter's arithmetic with the
+      // masks from s_mask; an aligned front or z = 0 reads an all-ones row, and
+      // an empty quarter's pieces are zeros already)
+      const uint32_t front = kQuarter - len - z; // < 1024 for a live body
+      const u32x4 mf = *reinterpret_cast<const u32x4 *>(s_mask + 4u * (front & 15u));
+      const u32x4 me = *reinterpret_cast<const u32x4 *>(s_mask + 64u + 4u * z);
+      const uint32_t e_front = (lane == lane_of_piece((front >> 4) & 63u)) ? 0u : 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t d = 0; d < 4; ++d)
+        buf[b][d] = and_or_keep(and_or_keep(buf[b][d], mf[d], e_front), me[d], e_end);
       zany |= z;
       zl = (hi == b) ? z : zl;
       const uint32_t sd = __builtin_amdgcn_readlane(m.seed, 4u * k + b);
