@@ -690,6 +690,10 @@ constexpr bool kRaggedAhead2 = RPCCRC_RAGGED_AHEAD2 != 0;
 #define RPCCRC_EARLY_ROW 1
 #endif
 constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
+#ifndef RPCCRC_LDS_MASKS
+#define RPCCRC_LDS_MASKS 1
+#endif
+constexpr bool kLdsMasks = RPCCRC_LDS_MASKS != 0;
 #ifndef RPCCRC_TWO_PHASE
 #define RPCCRC_TWO_PHASE 1
 #endif
@@ -779,7 +783,19 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // DYN control block (dyn_ring_words): task counter, done counts, slot
   // generations (slot s starts at round s), CRC ring.
   __shared__ uint32_t s_ctl[DYN ? (STEAL ? dyn_ctl_words(QB) : dyn_ring_words(QB)) : 1];
-  static_assert(sizeof(s_lds) + sizeof(s_ctl) <= kRowsLdsMax, "leave a CU room for the drop-in service");
+  // Ragged QB = 1 (RPCCRC_LDS_MASKS): the edge fixes' byte masks as a table, as
+  // crc32_small_kernel's s_mask (row f: bytes >= f of the first piece; row
+  // 16 + z: bytes below 16 - z of the last) -- 16 SALU per fix saved.
+  constexpr bool kMaskTab = kLdsMasks && QB == 1 && RAGGED && (ABL & kRowsAblNaturalOrder) == 0;
+  __shared__ __attribute__((aligned(16))) uint32_t s_mask[kMaskTab ? 128 : 4];
+  static_assert(sizeof(s_lds) + sizeof(s_ctl) + (kMaskTab ? sizeof(s_mask) : 0) <= kRowsLdsMax,
+                "leave a CU room for the drop-in service");
+  if constexpr (kMaskTab) {
+    if (threadIdx.x < 128u) {
+      const uint32_t t = threadIdx.x, k = (t >> 2) & 15u, d = t & 3u;
+      s_mask[t] = (t < 64u) ? keep_front_dword(k, d) : keep_end_dword(16u - k, d);
+    }
+  }
   // kEarlyRow: each wave's first task is static (DYN: counter index = wave, so
   // the LDS counter starts at 16), and its first row's loads are issued between
   // the image's global loads and its LDS stores -- the row's HBM latency then
@@ -1217,7 +1233,23 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
 #pragma unroll
         for (uint32_t b = 0; b < 4; ++b) {
           const uint32_t fb = front - b * kQuarter; // wraps (>= 1024) outside quarter b
-          fix_quarter<kNat>(buf[b], lane, fb, (b == 3 && last) ? z : 0u);
+          const uint32_t zb = (b == 3 && last) ? z : 0u;
+          if constexpr (kMaskTab) {
+            if ((fb & 15u) != 0u && fb < kQuarter) {
+              const u32x4 mf = *reinterpret_cast<const u32x4 *>(s_mask + 4u * (fb & 15u));
+              const uint32_t e = (lane == lane_of_piece(fb >> 4)) ? 0u : 0xFFFFFFFFu;
+#pragma unroll
+              for (uint32_t d = 0; d < 4; ++d) buf[b][d] = and_or_keep(buf[b][d], mf[d], e);
+            }
+            if (zb != 0u) {
+              const u32x4 me = *reinterpret_cast<const u32x4 *>(s_mask + 64u + 4u * zb);
+              const uint32_t e = (lane == lane_of_piece(63u)) ? 0u : 0xFFFFFFFFu;
+#pragma unroll
+              for (uint32_t d = 0; d < 4; ++d) buf[b][d] = and_or_keep(buf[b][d], me[d], e);
+            }
+          } else {
+            fix_quarter<kNat>(buf[b], lane, fb, zb);
+          }
         }
       }
     };
