@@ -100,6 +100,13 @@ def test_null_and_empty_need_no_device():
     assert _lib.rpc_crc32(b"abc", 2**32) == 0  # len mod 2^32 == 0
 
 
+def test_service_stop_without_a_service():
+    """rpc_crc32_service_stop with no drop-in service started (no device needed):
+    nothing to stop, RPCCRC_OK."""
+    import rpc_amd
+    assert rpc_amd.service_stop() == 0
+
+
 def test_test_library_exports_the_same_abi():
     """librpccrc_test.so (fault-injection build for the error-word tests) exports the
     same symbols; only it knows the test switch (the product library must
