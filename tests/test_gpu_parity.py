@@ -1073,3 +1073,26 @@ def test_drop_in_service_stop():
         assert sync_ms < 50.0, sync_ms  # (the service's own life cap is 20 ms)
     assert rpc_amd.service_stop() == 0  # nothing running
     assert rpc_amd.rpc_crc32(b"123456789") == 0xCBF43926
+
+
+@pytest.mark.parametrize("mb", [8, 24, 64])
+def test_two_phase_stealing_grid_sizes(mb):
+    """Two-phase tail stealing (round 5, crc32_rows.h rows_phase): phase 1 runs the
+    static rounds up to the claiming one, phase 2 the rest with the pool protocol.
+    With few workgroups (set_options max_blocks) the phase switch falls at other
+    round counts and pool sizes; every CRC of uniform one-row and four-per-row
+    batches and of a ragged batch must come out exact on each grid."""
+    rng = np.random.default_rng(900 + mb)
+    rpc_amd.set_options(max_blocks=mb)
+    try:
+        for n, L in ((8 * 32 * mb * 3 + 17, 256), (4 * 8 * 32 * mb * 2 + 5, 1024)):
+            host = oracle.splitmix_bytes(n * L, n ^ L)
+            got = u32(rpc_amd.device_uniform(to_dev(host), n, L))
+            assert np.array_equal(got, oracle.crc32_uniform(host, n, L)), (n, L)
+        n = 8 * 32 * mb * 2 + 9
+        lens = rng.integers(0, 9000, n).astype(np.uint32)
+        offs = _packed_offsets(lens, 3)
+        host = oracle.splitmix_bytes(int(lens.sum()) + 32, 901 + mb)
+        _ragged_check(host, offs, lens)
+    finally:
+        rpc_amd.set_options(max_blocks=0)
