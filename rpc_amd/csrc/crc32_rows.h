@@ -694,6 +694,14 @@ constexpr bool kEarlyRow = RPCCRC_EARLY_ROW != 0;
 #define RPCCRC_LDS_MASKS 1
 #endif
 constexpr bool kLdsMasks = RPCCRC_LDS_MASKS != 0;
+// Uniform QB = 1 batches through the ragged pipeline (loads two rows ahead,
+// chain of row C beside the merge of row P): A/B builds only.  Round 5, rotated,
+// one box: NS +0.8 %, C3 +0.6 %, C4 +1.5 % against the plain loop
+// (profiles/r05upipe; every uniform / stealing test green with it).
+#ifndef RPCCRC_UNIFORM_PIPE
+#define RPCCRC_UNIFORM_PIPE 0
+#endif
+constexpr bool kUniformPipe = RPCCRC_UNIFORM_PIPE != 0;
 #ifndef RPCCRC_TWO_PHASE
 #define RPCCRC_TWO_PHASE 1
 #endif
@@ -1712,7 +1720,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       // Ragged batches only: C2 -1.6 %, while uniform batches (north star
       // +-0.5 %, C4's chunks +0.6 %) keep the plain loop
       // (profiles/r02/r02r_rows_pipeline_ab.txt).
-      constexpr bool kPipe = kRowsPipe && RAGGED && !kTwoChains &&
+      constexpr bool kPipe = kRowsPipe && (RAGGED || kUniformPipe) && !kTwoChains &&
                              (ABL & (kRowsAblNoCompute | kRowsAblNoMerge | kRowsAblNoTranspose)) == 0;
       // Row C's chain (full / half / quarter row, rows::*_row_segs) and row P's
       // merge, inside each arm so the scheduler overlaps it with C's chain (P's
