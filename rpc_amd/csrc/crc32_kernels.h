@@ -187,13 +187,21 @@ constexpr uint32_t kSvcInline = 116;                   // bodies up to this leng
 // second PCIe round trip; longer bodies go to SvcShared::body.  The host writes
 // the bytes, then line 1's tag, then line 0's req word; the service takes an
 // inline request only when the XOR of the block's 32 dwords -- len, seq, the
-// 29 inline words, the tag -- is 0, i.e. the tag equals svc_tag(len, seq,
-// inline words).  A poll's dwords (one per lane) come back in pieces of the
-// memory system's choosing, in no set order; a poll that caught any piece
-// before the host's stores to it (a stale word next to a current req word, in
-// either line) shows a non-zero XOR with probability 1 - 2^-32 unless the stale
-// words equal the new ones, and is retried (round 4's tag checked
-// line 1 only, and relied on line 0 being read as one 64-B snapshot).
+// 29 inline words, the tag -- equals len ^ seq ^ svc_mix(len, seq), i.e. the
+// tag equals svc_tag(len, seq, inline words) = svc_mix(len, seq) ^ XOR(inline
+// words).  A poll's dwords (one per lane) come back in pieces of the memory
+// system's choosing, in no set order; a poll that caught any piece before the
+// host's stores to it (a stale word next to a current req word, in either
+// line) fails the check with probability 1 - 2^-32 unless the stale words
+// equal the new ones, and is retried (round 4's tag checked line 1
+// only, and relied on line 0 being read as one 64-B snapshot).
+// The mix (round 5's final pass): with a plain XOR tag (len ^ seq ^ inline
+// words), a poll that read the new req word beside the PREVIOUS request's
+// inline words and tag summed to len ^ seq ^ len' ^ seq', which is 0 whenever
+// the two (len, seq) pairs differ by the same bits -- e.g. len 4 -> 5 with seq
+// 7 -> 8 ... 6 -> 7 (seq changes by 1): one wrong CRC in ~30000 calls of the
+// 10-thread stress test (profiles/r05final6).  svc_mix is a bijection of
+// seq * C + len, so the previous request's words never pass for the new one.
 // Rounds 1-4 took the tag = seq.
 struct SvcReq {
   uint64_t req;
@@ -202,9 +210,18 @@ struct SvcReq {
 };
 static_assert(sizeof(SvcReq) == 128, "two lines per request block");
 static_assert(kSvcInline % 4 == 0, "inline bytes as whole words");
+// fmix32 (MurmurHash3's finalizer, a bijection) of seq * golden + len.
+__host__ __device__ inline uint32_t svc_mix(uint32_t len, uint32_t seq) {
+  uint32_t h = seq * 0x9E3779B1u + len;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
 // The tag of an inline request (host side; the service checks the XOR).
 inline uint32_t svc_tag(uint32_t len, uint32_t seq, const uint32_t *inl_words) {
-  uint32_t x = len ^ seq;
+  uint32_t x = svc_mix(len, seq);
   for (uint32_t k = 0; k < kSvcInline / 4; ++k) x ^= inl_words[k];
   return x;
 }

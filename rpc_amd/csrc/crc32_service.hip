@@ -166,8 +166,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
       const uint32_t xsum = (uint32_t)__builtin_amdgcn_readlane((int)xs, (int)(32 * i));
       if (lens[i] > kSvcMaxLen) lens[i] = kSvcMaxLen; // (the host never sends more)
       inl[i] = lens[i] <= kSvcInline;
-      // an inline request counts once the whole block is current (XOR 0)
-      pend[i] = seqs[i] != served[i] && (!inl[i] || xsum == 0u);
+      // an inline request counts once the whole block is current: the XOR of
+      // its 32 dwords is len ^ seq ^ svc_mix(len, seq) (crc32_kernels.h SvcReq)
+      pend[i] = seqs[i] != served[i] && (!inl[i] || xsum == (lens[i] ^ seqs[i] ^ svc_mix(lens[i], seqs[i])));
       any = any || pend[i];
     }
     if (any) {
