@@ -702,6 +702,10 @@ constexpr bool kLdsMasks = RPCCRC_LDS_MASKS != 0;
 #define RPCCRC_UNIFORM_PIPE 0
 #endif
 constexpr bool kUniformPipe = RPCCRC_UNIFORM_PIPE != 0;
+#ifndef RPCCRC_RAGGED_Q3_TEMPORAL
+#define RPCCRC_RAGGED_Q3_TEMPORAL 0
+#endif
+constexpr bool kRaggedQ3Temporal = RPCCRC_RAGGED_Q3_TEMPORAL != 0;
 #ifndef RPCCRC_TWO_PHASE
 #define RPCCRC_TWO_PHASE 1
 #endif
@@ -1158,7 +1162,13 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         }
         const __amdgpu_buffer_rsrc_t row = row_rsrc(base);
 #pragma unroll
-        for (int b = 0; b < 4; ++b) buf[b] = ldb16<NT>(row, off[b]);
+        for (int b = 0; b < 4; ++b) {
+          // RPCCRC_RAGGED_Q3_TEMPORAL (A/B): a ragged row's last quarter through
+          // L2 at normal priority, so the line it shares with the next row
+          // (rows end at the body's 16-B end) is there when that row loads it
+          if (RAGGED && kRaggedQ3Temporal && b == 3) buf[b] = ldb16<false>(row, off[b]);
+          else buf[b] = ldb16<NT>(row, off[b]);
+        }
       }
     };
     uint32_t W = 0; // running crc0 (Horner over rows) of the current item, wave-uniform
