@@ -21,6 +21,8 @@
 #include <algorithm>
 
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "crc32_gf2.h"
 #include "crc32_kernels.h"
@@ -502,9 +504,9 @@ hipError_t launch_packed_batch(const PackedBatch &p, bool nt, int max_blocks, hi
 // ---------------------------------------------------------------------------
 // Split ragged batches: bodies whose bytes plus 16-B end pad fit a 1 KiB
 // quarter ("small") go four to a row through the QB = 4 rows kernel, the rest
-// one body per row sequence (QB = 1).  Flags, their exclusive scan (rocPRIM)
-// and an order-preserving scatter build both lists and their counts on the
-// device (no host round trip); each rows kernel reads its count from the
+// one body per row sequence (QB = 1).  An exclusive scan (rocPRIM) of the small
+// flags, computed as it reads them, and an order-preserving scatter build both
+// lists and their counts on the device (no host round trip); each rows kernel reads its count from the
 // device and writes CRC i to out[idx[i]].  Frames batches (bodies <= 1 KiB,
 // rpc.h:17) take this path: almost every body is small.
 // ---------------------------------------------------------------------------
@@ -515,23 +517,33 @@ __device__ __forceinline__ bool small_body(const uint8_t *base, uint64_t off, ui
   return len + z <= 1024u;
 }
 
-__global__ void __launch_bounds__(256) split_flag_kernel(const uint8_t *base, const uint64_t *offsets,
-                                                         const uint32_t *lengths, uint64_t n, uint32_t *flag) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (i < n) flag[i] = small_body(base, offsets[i], lengths[i]) ? 1u : 0u;
-}
+// Item i's small flag, computed where the scan reads it (round 5: the flags
+// were a kernel and an array of their own, 5 us and a launch per call).
+struct SmallFlag {
+  const uint8_t *base;
+  const uint64_t *offsets;
+  const uint32_t *lengths;
+  __host__ __device__ uint32_t operator()(uint64_t i) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return small_body(base, offsets[i], lengths[i]) ? 1u : 0u;
+#else
+    return 0u; // (the host never evaluates it)
+#endif
+  }
+};
+using SmallFlags = rocprim::transform_iterator<rocprim::counting_iterator<uint64_t>, SmallFlag, uint32_t>;
 
 // Item i goes to slot pos[i] of the small list or slot i - pos[i] of the big
 // one (stable: both lists keep batch order, so consecutive tasks stay
 // neighbours in memory).  Thread n - 1 publishes both counts.
-__global__ void __launch_bounds__(256) split_scatter_kernel(const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
-                                                            const uint32_t *flag, const uint32_t *pos,
+__global__ void __launch_bounds__(256) split_scatter_kernel(const uint8_t *base, const uint64_t *offsets,
+                                                            const uint32_t *lengths, uint64_t n, const uint32_t *pos,
                                                             SplitLists l) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
-  const uint32_t f = flag[i], p = pos[i];
   const uint64_t off = offsets[i];
   const uint32_t len = lengths[i];
+  const uint32_t f = small_body(base, off, len) ? 1u : 0u, p = pos[i];
   if (f) {
     l.s_off[p] = off;
     l.s_len[p] = len;
@@ -548,8 +560,9 @@ __global__ void __launch_bounds__(256) split_scatter_kernel(const uint64_t *offs
   }
 }
 
-hipError_t split_scan(void *tmp, size_t &bytes, const uint32_t *flag, uint32_t *pos, uint64_t n, hipStream_t s) {
-  return rocprim::exclusive_scan(tmp, bytes, flag, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
+hipError_t split_scan(void *tmp, size_t &bytes, const SmallFlag &f, uint32_t *pos, uint64_t n, hipStream_t s) {
+  const SmallFlags flags(rocprim::counting_iterator<uint64_t>(0), f);
+  return rocprim::exclusive_scan(tmp, bytes, flags, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
 }
 } // namespace
 
@@ -582,9 +595,9 @@ hipError_t launch_small(const ItemsArgs &a, bool nt, int max_blocks, hipStream_t
 
 hipError_t split_workspace_bytes(uint64_t n, size_t *bytes) {
   size_t scan = 0;
-  const hipError_t e = split_scan(nullptr, scan, nullptr, nullptr, n, nullptr);
+  const hipError_t e = split_scan(nullptr, scan, SmallFlag{}, nullptr, n, nullptr);
   if (e != hipSuccess) return e;
-  *bytes = 2 * align256(n * 4) + align256(16) + 2 * (align256(n * 8) + 2 * align256(n * 4)) + align256(scan);
+  *bytes = align256(n * 4) + align256(16) + 2 * (align256(n * 8) + 2 * align256(n * 4)) + align256(scan);
   return hipSuccess;
 }
 
@@ -599,7 +612,6 @@ hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes,
     w += align256(bytes);
     return r;
   };
-  uint32_t *flag = reinterpret_cast<uint32_t *>(take(n * 4));
   uint32_t *pos = reinterpret_cast<uint32_t *>(take(n * 4));
   SplitLists l;
   l.counts = reinterpret_cast<uint64_t *>(take(16));
@@ -613,12 +625,9 @@ hipError_t launch_split_batch(const ItemsArgs &proto, void *ws, size_t ws_bytes,
   if (used > ws_bytes) return hipErrorInvalidValue;
   size_t scan = ws_bytes - used;
   const dim3 g((unsigned)((n + 255) / 256));
-  hipLaunchKernelGGL(split_flag_kernel, g, dim3(256), 0, s, proto.base, proto.offsets, proto.lengths, n, flag);
-  hipError_t e = hipGetLastError();
+  hipError_t e = split_scan(w, scan, SmallFlag{proto.base, proto.offsets, proto.lengths}, pos, n, s);
   if (e != hipSuccess) return e;
-  e = split_scan(w, scan, flag, pos, n, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(split_scatter_kernel, g, dim3(256), 0, s, proto.offsets, proto.lengths, n, flag, pos, l);
+  hipLaunchKernelGGL(split_scatter_kernel, g, dim3(256), 0, s, proto.base, proto.offsets, proto.lengths, n, pos, l);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   ItemsArgs a = proto; // small bodies, four per row
