@@ -243,11 +243,13 @@ static double env_frac(const char *name, double dflt) {
 // profiles/r05v) and no larger: C2 rotated A/B on one box, no pool 6073 / 6100
 // / 6102 us, 2 % 6069 / 6078 / 6087, 3 % 6041 / 6048 / 6069, 5 % 6052 / 6076 /
 // 6079, 8 % 6046 / 6064 / 6066 (profiles/r05x, r05z).
-// Uniform QB = 1 (NS, C3, C4's chunks) 5 % since the two-phase loop: NS
-// 593.0 / 594.3 us against 597.5 / 599.8 with 8 %, C4 the same, 3 % +1-2 %
-// (rotated, profiles/r05zb); QB = 4 (C1) keeps 8 % (5 % +1-3 %, 3 % +4-7 %).
+// Uniform QB = 1 (NS, C3, C4's chunks) 6.5 % since the two-phase loop.  Rotated
+// A/Bs on three boxes: 5 % beat 8 % on one (NS 593.0 / 594.3 against 597.5 /
+// 599.8 us, profiles/r05zb), 6.5 % beat 5 % on the next (NS 596.6-598.1 against
+// 601.1-608.1, C4 the same, 4 % worse; r05frac) and matched 8 % on the third
+// (r05frac2); 3 % cost 1-2 %.  QB = 4 (C1) keeps 8 % (5 % +1-3 %, 3 % +4-7 %).
 static double steal_frac(int QB = 1, bool ragged = false) {
-  static const double f1 = env_frac("RPCCRC_STEAL_FRAC", 0.05);
+  static const double f1 = env_frac("RPCCRC_STEAL_FRAC", 0.065);
   static const double f4 = env_frac("RPCCRC_STEAL_FRAC_QB4", 0.08);
   static const double fr = env_frac("RPCCRC_STEAL_FRAC_RAGGED", 0.03);
   return QB == 4 ? f4 : ragged ? fr : f1;
