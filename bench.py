@@ -580,7 +580,8 @@ def live_traffic(args, algo_bytes: int):
     corrected as that guide says: gfx950 FETCH_SIZE counts half the bytes of a
     wide streaming read (x 2), both are in KiB (x 1024).  The rows kernel also
     runs tiny launches (the big-body route's empty chunk pass): only dispatches
-    within half of the largest count.  Falls back to the committed summary."""
+    whose FETCH_SIZE is within half of the largest, the median over them.  Falls
+    back to the committed summary."""
     import csv
     import glob
     import shutil
@@ -593,6 +594,7 @@ def live_traffic(args, algo_bytes: int):
         return None, "rocprofv3 not found"
     tmp = tempfile.mkdtemp(prefix="rpccrc_pmc_")
     vals = {}
+    seq = {}
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, counter)
@@ -613,8 +615,21 @@ def live_traffic(args, algo_bytes: int):
                         per[(f, r["Dispatch_Id"])] = per.get((f, r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
             if not per:
                 return None, f"no {counter} rows for crc32_rows_kernel"
-            v = sorted(per.values())
-            vals[counter] = statistics.median([x for x in v if x >= 0.5 * v[-1]])
+            seq[counter] = [per[k] for k in sorted(per, key=lambda k: (k[0], int(k[1])))]
+        # The big launches are picked on FETCH_SIZE (the stream's reads, the same
+        # on every launch), by position in launch order, and the same positions
+        # are read from the WRITE_SIZE pass: one launch that writes back dirty
+        # lines the on-device generator left (a write outlier) then cannot
+        # displace the others, as a filter on the write values themselves would.
+        f = seq["FETCH_SIZE"]
+        big = [i for i, x in enumerate(f) if x >= 0.5 * max(f)]
+        vals["FETCH_SIZE"] = statistics.median([f[i] for i in big])
+        w = seq["WRITE_SIZE"]
+        if len(w) == len(f):
+            vals["WRITE_SIZE"] = statistics.median([w[i] for i in big])
+        else:
+            w = sorted(w)
+            vals["WRITE_SIZE"] = statistics.median([x for x in w if x >= 0.5 * w[len(w) // 2]])
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     hbm = 2.0 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024
