@@ -573,6 +573,25 @@ def load_traffic(cfg: str):
         return None
 
 
+def pick_launch_traffic(fetch, write):
+    """Per-launch (FETCH_SIZE, WRITE_SIZE) from two PMC passes' per-dispatch
+    values in launch order.  The big launches are picked on FETCH_SIZE (the
+    stream's reads, the same on every launch), within half of the largest, and
+    the same positions are read from the WRITE_SIZE pass; medians over them.  A
+    few launches that write back dirty lines left by the on-device generator
+    (write outliers) then cannot displace the others, as a filter on the write
+    values themselves would (profiles/r05final10).  If the passes saw different
+    launch counts, the writes are filtered on half their own median."""
+    import statistics
+
+    big = [i for i, x in enumerate(fetch) if x >= 0.5 * max(fetch)]
+    f = statistics.median([fetch[i] for i in big])
+    if len(write) == len(fetch):
+        return f, statistics.median([write[i] for i in big])
+    w = sorted(write)
+    return f, statistics.median([x for x in w if x >= 0.5 * w[len(w) // 2]])
+
+
 def live_traffic(args, algo_bytes: int):
     """HBM bytes per launch of the dominant kernel, measured in this run: two
     rocprofv3 PMC passes (FETCH_SIZE, then WRITE_SIZE -- separate runs, as
@@ -585,7 +604,6 @@ def live_traffic(args, algo_bytes: int):
     import csv
     import glob
     import shutil
-    import statistics
     import subprocess
     import tempfile
 
@@ -616,20 +634,7 @@ def live_traffic(args, algo_bytes: int):
             if not per:
                 return None, f"no {counter} rows for crc32_rows_kernel"
             seq[counter] = [per[k] for k in sorted(per, key=lambda k: (k[0], int(k[1])))]
-        # The big launches are picked on FETCH_SIZE (the stream's reads, the same
-        # on every launch), by position in launch order, and the same positions
-        # are read from the WRITE_SIZE pass: one launch that writes back dirty
-        # lines the on-device generator left (a write outlier) then cannot
-        # displace the others, as a filter on the write values themselves would.
-        f = seq["FETCH_SIZE"]
-        big = [i for i, x in enumerate(f) if x >= 0.5 * max(f)]
-        vals["FETCH_SIZE"] = statistics.median([f[i] for i in big])
-        w = seq["WRITE_SIZE"]
-        if len(w) == len(f):
-            vals["WRITE_SIZE"] = statistics.median([w[i] for i in big])
-        else:
-            w = sorted(w)
-            vals["WRITE_SIZE"] = statistics.median([x for x in w if x >= 0.5 * w[len(w) // 2]])
+        vals["FETCH_SIZE"], vals["WRITE_SIZE"] = pick_launch_traffic(seq["FETCH_SIZE"], seq["WRITE_SIZE"])
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     hbm = 2.0 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024

@@ -90,3 +90,26 @@ def test_gpus2_per_rank_crc_check():
     assert bad["ranks_crc_ok"] is False
     c = bad["ranks_crc_check"]
     assert c["ranks_ok"] == 1 and c["mismatches"] == 1 and c["bodies_checked"] == 128
+
+
+def test_live_traffic_launch_selection():
+    """bench.py's live-traffic reading (pick_launch_traffic): the big launches are
+    chosen on FETCH_SIZE and the same launch positions are read from WRITE_SIZE, so a
+    few write outliers (dirty lines written back during one launch, r05final10) or
+    the big-body route's tiny launches do not stand for the product's launches."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    fetch = [2097487.0, 2097463.0, 2097462.0, 2097462.0, 12.0, 2097462.0]
+    write = [159499.0, 160001.0, 4185.0, 4186.0, 90.0, 4185.0]
+    f, w = bench.pick_launch_traffic(fetch, write)
+    assert (f, w) == (2097462.0, 4186.0)
+    # an outlier on a minority of launches does not move the median
+    f, w = bench.pick_launch_traffic([100.0] * 5, [9000.0, 10.0, 10.0, 10.0, 9000.0])
+    assert (f, w) == (100.0, 10.0)
+    # the tiny launches are left out of both
+    f, w = bench.pick_launch_traffic([100.0, 1.0, 1.0, 100.0, 1.0], [10.0, 0.0, 0.0, 10.0, 0.0])
+    assert (f, w) == (100.0, 10.0)
+    # different launch counts between the passes: writes within half their median
+    f, w = bench.pick_launch_traffic([100.0, 100.0], [10.0, 10.0, 1.0, 10.0])
+    assert (f, w) == (100.0, 10.0)
