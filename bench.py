@@ -759,9 +759,17 @@ def main():
 
     if world != args.gpus:
         print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
-    # one process per GPU; ranks beyond the visible GPUs (a gloo rehearsal on
-    # a 1-GPU box) share them
-    dev_index = local_rank % max(1, torch.cuda.device_count())
+    # one process per GPU.  RCCL refuses two ranks on one GPU, so with the nccl
+    # backend more local ranks than visible GPUs is an error, stated before any
+    # process group exists; ranks beyond the visible GPUs
+    # (a gloo rehearsal on a 1-GPU box) share them
+    ndev = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if args.dist_backend == "nccl" and local_world > ndev:
+        print(f"bench: {local_world} ranks on this node but {ndev} visible GPU(s): the nccl (RCCL) backend needs "
+              f"one GPU per rank (use --gpus <= {ndev}, or --dist-backend gloo to share GPUs)", file=sys.stderr)
+        sys.exit(2)
+    dev_index = local_rank % max(1, ndev)
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     dist = None
@@ -912,9 +920,16 @@ def main():
                 # same buffer on the same GPU, measured in this run: the rows
                 # kernel's own dealing and loads with no CRC work, in blocks
                 # alternating with blocks of product steps (stream_read_probe)
+                # (both numerators, named) -- the interleaved
+                # product blocks (same protocol and clock as the probe's) and
+                # the headline achieved rate of the timed region
                 "frac_of_stream_read": (round(extra["stream_read_probe"]["product_interleaved_GBps"]
                                               / extra["stream_read_probe"]["rows_dealing_GBps"], 4)
                                         if "product_interleaved_GBps" in extra.get("stream_read_probe", {}) else None),
+                "frac_of_stream_read_numerator": "product_interleaved_GBps",
+                "frac_of_stream_read_achieved": (round(w.algo_bytes / tr["kernel_s"] / 1e9
+                                                       / extra["stream_read_probe"]["rows_dealing_GBps"], 4)
+                                                 if "rows_dealing_GBps" in extra.get("stream_read_probe", {}) else None),
             },
             # the reference crc.c on the host's cores: timed on rank 0 at N = 1 only
             # (an N > 1 run shares the host among N ranks)

@@ -294,6 +294,24 @@ RPCCRC_API int rpc_crc32_device_clear_status(void);
  * serves calls as usual).  Not part of crc.h; the reference has no counterpart. */
 RPCCRC_API int rpc_crc32_service_stop(void);
 
+/* Counters of the drop-in service, summed over every device this process has
+ * used (no device needed; all zero before the first drop-in call).  A request
+ * that gets no answer in 2 s is given up and the call launches a kernel
+ * instead; after that, while the device's latest service instance has not
+ * started (queued behind other kernels), drop-in calls launch a kernel without
+ * posting (`bypassed`), and posted calls wait 2 ms, not 2 s (`fallbacks_short`),
+ * until one is answered again.  Not part of crc.h. */
+typedef struct rpccrc_service_stats {
+  uint64_t services;        /* devices with a drop-in service */
+  uint64_t running;         /* of them, with an instance running or queued */
+  uint64_t launched;        /* instances launched */
+  uint64_t answered;        /* drop-in calls the service answered */
+  uint64_t fallbacks_full;  /* requests given up after the full 2-s wait */
+  uint64_t fallbacks_short; /* requests given up after the 2-ms wait that follows a give-up */
+  uint64_t bypassed;        /* calls that did not post (instance not started after a give-up) */
+} rpccrc_service_stats_t;
+RPCCRC_API int rpc_crc32_service_stats(rpccrc_service_stats_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -303,6 +303,15 @@ def service_stop() -> int:
     return int(_lib.rpc_crc32_service_stop())
 
 
+def service_stats() -> dict:
+    """The drop-in service's counters over every device this process used
+    (rpccrc_service_stats_t): services, running, launched, answered,
+    fallbacks_full, fallbacks_short, bypassed."""
+    st = _lib.ServiceStats()
+    check(_lib.rpc_crc32_service_stats(ctypes.byref(st)), "rpc_crc32_service_stats")
+    return {k: int(getattr(st, k)) for k, _ in st._fields_}
+
+
 def device_info() -> str:
     buf = ctypes.create_string_buffer(256)
     check(_lib.rpc_crc32_device_info(buf, 256), "rpc_crc32_device_info")

@@ -82,6 +82,15 @@ rpc_crc32_device_status = _sig("rpc_crc32_device_status", _i32)
 rpc_crc32_device_clear_status = _sig("rpc_crc32_device_clear_status", _i32)
 rpc_crc32_service_stop = _sig("rpc_crc32_service_stop", _i32)
 
+
+class ServiceStats(ctypes.Structure):
+    """rpccrc_service_stats_t (include/rpccrc.h)."""
+    _fields_ = [(k, ctypes.c_uint64) for k in ("services", "running", "launched", "answered", "fallbacks_full",
+                                               "fallbacks_short", "bypassed")]
+
+
+rpc_crc32_service_stats = _sig("rpc_crc32_service_stats", _i32, ctypes.POINTER(ServiceStats))
+
 #: Every symbol include/rpccrc.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "rpc_crc32",
@@ -111,6 +120,7 @@ EXPORTS = (
     "rpc_crc32_device_status",
     "rpc_crc32_device_clear_status",
     "rpc_crc32_service_stop",
+    "rpc_crc32_service_stats",
 )
 
 

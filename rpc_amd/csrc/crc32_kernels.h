@@ -178,65 +178,43 @@ constexpr uint32_t kSvcWaves = 8;                      // waves of the service w
 constexpr uint32_t kSvcPer = 2;                        // slots per wave: wave w owns slots w + 8 i
 constexpr uint32_t kSvcSlots = kSvcWaves * kSvcPer;    // concurrent drop-in calls served
 constexpr uint32_t kSvcMaxLen = 1024;                  // MAX_BODY_LEN (rpc.h:17)
-constexpr uint32_t kSvcStop = 0, kSvcExited = 1;       // SvcShared::ctl words
+constexpr uint32_t kSvcStop = 0, kSvcExited = 1, kSvcStarted = 2; // SvcShared::ctl words
 constexpr uint32_t kSvcInline = 116;                   // bodies up to this length travel in the request block
 // A slot's request block: two 64-B lines the service reads in ONE poll.
 //   line 0: req = {len (low), seq (high)}, then inline bytes 0..55
 //   line 1: inline bytes 56..115, then tag
 // An inline body (len <= kSvcInline) ends at inline byte 116, so its CRC needs no
 // second PCIe round trip; longer bodies go to SvcShared::body.  The host writes
-// the bytes, then line 1's tag, then line 0's req word; the service takes an
-// inline request only when the XOR of the block's 32 dwords -- len, seq, the
-// 29 inline words, the tag -- equals len ^ seq ^ svc_mix(len, seq), i.e. the
-// tag equals svc_tag(len, seq, inline words) = svc_mix(len, seq) ^ XOR(inline
-// words).  A poll's dwords (one per lane) come back in pieces of the memory
-// system's choosing, in no set order; a poll that caught any piece before the
-// host's stores to it (a stale word next to a current req word, in either
-// line) fails the check with probability 1 - 2^-32 unless the stale words
-// equal the new ones, and is retried (round 4's tag checked line 1
-// only, and relied on line 0 being read as one 64-B snapshot).
-// The mix (round 5's final pass): with a plain XOR tag (len ^ seq ^ inline
-// words), a poll that read the new req word beside the PREVIOUS request's
-// inline words and tag summed to len ^ seq ^ len' ^ seq', which is 0 whenever
-// the two (len, seq) pairs differ by the same bits -- e.g. len 4 -> 5 with seq
-// 7 -> 8 ... 6 -> 7 (seq changes by 1): one wrong CRC in ~30000 calls of the
-// 10-thread stress test (profiles/r05final6).  svc_mix is a bijection of
-// seq * C + len, so the previous request's words never pass for the new one.
-// Rounds 1-4 took the tag = seq.
+// the bytes, then line 1's tag, then line 0's req word.
+// Check (round 6, crc32_service_math.h word_hash): tag = XOR over the block's
+// dwords 0..30 (len, seq, the 29 inline words) of word_hash(dword, position),
+// XOR -- for a longer body -- the same sum over every masked word of the body's
+// virtual buffer (svc::body_sum).  The service answers a request only when its
+// own sum over what it read equals the tag it read: a poll or body read that
+// combined stale and current words (its pieces arrive in an order the memory
+// system chooses) fails with probability 1 - 2^-32 whatever the bodies, and is
+// retried.  Rounds 4-5 summed the words with a plain XOR (and mixed only len and
+// seq): two stale words with equal old -> new deltas cancelled, and requests over
+// 116 B had no check at all.
 struct SvcReq {
   uint64_t req;
   uint8_t inl[kSvcInline];
   uint32_t tag;
 };
 static_assert(sizeof(SvcReq) == 128, "two lines per request block");
-static_assert(kSvcInline % 4 == 0, "inline bytes as whole words");
-// fmix32 (MurmurHash3's finalizer, a bijection) of seq * golden + len.
-__host__ __device__ inline uint32_t svc_mix(uint32_t len, uint32_t seq) {
-  uint32_t h = seq * 0x9E3779B1u + len;
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  return h ^ (h >> 16);
-}
-// The tag of an inline request (host side; the service checks the XOR).
-inline uint32_t svc_tag(uint32_t len, uint32_t seq, const uint32_t *inl_words) {
-  uint32_t x = svc_mix(len, seq);
-  for (uint32_t k = 0; k < kSvcInline / 4; ++k) x ^= inl_words[k];
-  return x;
-}
+static_assert(kSvcInline % 4 == 0 && kSvcInline / 4 == 29, "inline bytes as 29 whole words");
 struct SvcShared {
   // one block per slot (a shared line was written by up to 8 caller threads
   // while 8 waves polled it: 10 callers took 30 us a call, r04c)
   SvcReq rq[kSvcSlots];
   uint64_t res[kSvcSlots][8];         // device: {crc, seq} (crc in the low half), one 64-B line per slot
-  uint32_t ctl[16];                   // [kSvcStop] host: leave now; [kSvcExited] device: last instance that left
+  uint32_t ctl[16];                   // [kSvcStop] host: leave now; [kSvcExited] / [kSvcStarted] device: last instance that left / started
   uint8_t body[kSvcSlots][kSvcMaxLen]; // host: the body, right-aligned in 64 * seg bytes (seg 4 / 8 / 16)
 };
 // kshift: 3 x 64 words, kshift[c][L] = x^(8 * seg_c * (63 - L)) mod P for seg 4, 8, 16.
 // The kernel leaves after idle_ticks (s_memrealtime, 100 MHz) without a
-// request or after life_ticks in all; it then stores `instance` into
-// ctl[kSvcExited].
+// request or after life_ticks in all; it stores `instance` into
+// ctl[kSvcStarted] when it starts and into ctl[kSvcExited] when it leaves.
 hipError_t launch_service(SvcShared *sh, const uint32_t *tq, const uint32_t *kshift, uint64_t idle_ticks,
                           uint64_t life_ticks, uint32_t instance, hipStream_t stream);
 

@@ -18,11 +18,12 @@
 //          rq[slot].req = {len, seq} as ONE 64-bit store (x86 stores stay in order);
 //   wave   polls the request blocks of its kSvcPer slots (one dword per lane,
 //          both blocks in one round trip); a seq it has not answered is a
-//          request (inline: once the XOR of the block's dwords is 0, i.e.
-//          the tag matches every word polled -- SvcReq).  An inline body is
-//          already in registers; a longer one is read (every lane its seg bytes;
-//          the loads of all its pending slots in flight together).  It computes
-//          the CRC and stores {crc, seq} into res[slot] (one 64-bit store);
+//          request once its check sum matches the tag (crc32_kernels.h SvcReq:
+//          a non-linear, position-dependent sum over every word used).  An
+//          inline body is already in registers; a longer one is read (every
+//          lane its seg bytes; the loads of all its pending slots in flight
+//          together) and its words enter the sum.  It computes the CRC and
+//          stores {crc, seq} into res[slot] (one 64-bit store);
 //   host   spins on res[slot] until the seq matches.
 // The waves share the time of the last request in LDS (4 bytes) and all leave
 // after idle_ticks without one, after the kernel's lifetime cap, or when the
@@ -91,18 +92,30 @@ __device__ __forceinline__ Body load_body(const uint8_t *body, uint32_t seg, uin
 }
 
 // crc0 of V: the lane's chain over its seg / 4 words (bytes before the body
-// masked), shifted to V's end by the lane's constant, XORed over the wave.
-__device__ __forceinline__ uint32_t body_crc0(const Body &b, uint32_t seg, uint32_t len, uint32_t lane,
+// masked), shifted to V's end by the lane's constant, XORed over the wave; and
+// the request check's sum over the same masked words (svc::word_hash at
+// position kHashBodyPos + word index, XORed over the wave).
+struct BodySums {
+  uint32_t c0, h;
+};
+__device__ __forceinline__ BodySums body_crc0(const Body &b, uint32_t seg, uint32_t len, uint32_t lane,
                                               uint32_t kshift) {
   const uint32_t off0 = 64u * seg - len; // V offset of the body's first byte
-  uint32_t s = 0;
+  uint32_t s = 0, h = 0;
 #pragma unroll
   for (uint32_t d = 0; d < 4; ++d)
-    if (4u * d < seg) s = svc::crc0_word(s ^ (b.w[d] & svc::keep_mask(lane * seg + 4u * d, off0)));
+    if (4u * d < seg) {
+      const uint32_t w = b.w[d] & svc::keep_mask(lane * seg + 4u * d, off0);
+      s = svc::crc0_word(s ^ w);
+      h ^= svc::word_hash(w, svc::kHashBodyPos + lane * (seg >> 2) + d);
+    }
   s = svc::mulmod(s, kshift);
 #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) s ^= (uint32_t)__shfl_xor((int)s, m, 64);
-  return s;
+  for (int m = 1; m < 64; m <<= 1) {
+    s ^= (uint32_t)__shfl_xor((int)s, m, 64);
+    h ^= (uint32_t)__shfl_xor((int)h, m, 64);
+  }
+  return BodySums{s, h};
 }
 
 __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void crc32_service_kernel(
@@ -121,6 +134,9 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     s_last = (uint32_t)t_start;
     s_alive = kSvcWaves;
     s_leave = 0u;
+    // the host sees this instance running (a vector store): until then, after a
+    // request that went unanswered, its calls take the launch path
+    __hip_atomic_store(&sh->ctl[kSvcStarted], instance, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   for (uint32_t k = threadIdx.x; k <= kSvcInline; k += 64 * kSvcWaves) s_tq[k] = tq[k];
   __syncthreads();
@@ -146,29 +162,32 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
     // keep the instance alive while the departed wave's slots went unanswered)
     if (__hip_atomic_load(&s_leave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
     const uint32_t pv = ld_sys32(pblk); // both blocks, one round trip
-    // XOR of each block's 32 dwords (lanes 32 i .. 32 i + 31): 0 for a whole,
-    // current inline request (crc32_kernels.h SvcReq)
-    uint32_t xs = pv ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)pv, 0xB1, 0xF, 0xF, true); // quad_perm [1,0,3,2]
-    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x4E, 0xF, 0xF, true);              // quad_perm [2,3,0,1]
-    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x124, 0xF, 0xF, true);             // row_ror:4
-    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x128, 0xF, 0xF, true);             // row_ror:8
+    // the request check (crc32_kernels.h SvcReq): lane 32 i + d hashes block
+    // dword d at position d (d < 31), lane 32 i + 31 holds the tag as read; the
+    // XOR over each block's 32 lanes is 0 for a whole, current inline request
+    const uint32_t bd = lane & 31u;
+    uint32_t xs = bd == 31u ? pv : svc::word_hash(pv, bd);
+    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x124, 0xF, 0xF, true); // row_ror:4
+    xs ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)xs, 0x128, 0xF, 0xF, true); // row_ror:8
     {
       const auto sw = __builtin_amdgcn_permlane16_swap(xs, xs, false, false); // lane bit 4
       xs = sw[0] ^ sw[1];
     }
-    uint32_t lens[kSvcPer], seqs[kSvcPer];
+    uint32_t lens[kSvcPer], seqs[kSvcPer], xsum[kSvcPer];
     bool pend[kSvcPer], inl[kSvcPer];
     bool any = false;
 #pragma unroll
     for (uint32_t i = 0; i < kSvcPer; ++i) {
       lens[i] = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 0));
       seqs[i] = (uint32_t)__builtin_amdgcn_readlane((int)pv, (int)(32 * i + 1));
-      const uint32_t xsum = (uint32_t)__builtin_amdgcn_readlane((int)xs, (int)(32 * i));
-      if (lens[i] > kSvcMaxLen) lens[i] = kSvcMaxLen; // (the host never sends more)
+      xsum[i] = (uint32_t)__builtin_amdgcn_readlane((int)xs, (int)(32 * i));
+      if (lens[i] > kSvcMaxLen) lens[i] = kSvcMaxLen; // (the host never sends more; the check then fails)
       inl[i] = lens[i] <= kSvcInline;
-      // an inline request counts once the whole block is current: the XOR of
-      // its 32 dwords is len ^ seq ^ svc_mix(len, seq) (crc32_kernels.h SvcReq)
-      pend[i] = seqs[i] != served[i] && (!inl[i] || xsum == (lens[i] ^ seqs[i] ^ svc_mix(lens[i], seqs[i])));
+      // an inline request counts once its block's sum matches; a longer one is
+      // read first and counts once the block's and the body's sums match the tag
+      pend[i] = seqs[i] != served[i] && (!inl[i] || xsum[i] == 0u);
       any = any || pend[i];
     }
     if (any) {
@@ -192,8 +211,11 @@ __global__ __launch_bounds__(64 * kSvcWaves) __attribute__((amdgpu_waves_per_eu(
       for (uint32_t i = 0; i < kSvcPer; ++i) {
         if (!pend[i]) continue;
         const uint32_t len = lens[i], seg = svc::seg_of(len);
-        const uint32_t c0 = body_crc0(body[i], seg, len, lane, seg == 4u ? k4 : seg == 8u ? k8 : k16);
-        const uint32_t crc = len == 0u ? 0u : ~((inl[i] ? s_tq[len] : tq[len]) ^ c0);
+        const BodySums bs = body_crc0(body[i], seg, len, lane, seg == 4u ? k4 : seg == 8u ? k8 : k16);
+        // a longer body: its words as read must match the tag too (a torn
+        // {len, seq} pair or body read fails here; the next poll retries)
+        if (!inl[i] && (xsum[i] ^ bs.h) != 0u) continue;
+        const uint32_t crc = len == 0u ? 0u : ~((inl[i] ? s_tq[len] : tq[len]) ^ bs.c0);
         if (lane == 0)
           __hip_atomic_store(&sh->res[wave + kSvcWaves * i][0], (uint64_t)crc | ((uint64_t)seqs[i] << 32),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -314,9 +314,16 @@ struct Service {
   std::atomic<uint32_t> busy{0};
   uint32_t seq[kSvcSlots] = {}; // last request seq of each slot (written by the slot's holder)
   // Host copy of each slot's inline bytes (kSvcInline, as the request block holds
-  // them): the tag's checksum covers all of them (svc_tag), and reading them back
-  // from the coherent (uncached) block would cost a PCIe-speed read per word.
+  // them): the tag's check sum covers all of them (svc::block_sum), and reading
+  // them back from the coherent (uncached) block would cost a PCIe-speed read per word.
   uint32_t inl[kSvcSlots][kSvcInline / 4] = {};
+  // Set when a request was given up (no answer in kSvcWaitNs), cleared by the
+  // next answered one.  While set, a call whose instance has not started yet
+  // (still queued behind other kernels) takes the launch path without posting,
+  // and a posted call waits kSvcWaitShortNs, not kSvcWaitNs (one
+  // slow call, not a 2-s stall per call).
+  std::atomic<bool> degraded{false};
+  std::atomic<uint64_t> answered{0}, fallbacks_full{0}, fallbacks_short{0}, bypassed{0};
   bool ok = false;
 };
 
@@ -1080,10 +1087,14 @@ constexpr uint64_t kSvcLifeTicks = 2000000;  // 20 ms per instance: bounds what 
 // stream, and surfaces a real device error).  The abandoned request is safe to
 // leave: nobody waits for its seq, and the slot's next request carries a new one.
 constexpr uint64_t kSvcWaitNs = 2000000000;
+// After a request was given up, the next posted calls wait this long (the
+// instance has started by then, so an answer normally takes microseconds).
+constexpr uint64_t kSvcWaitShortNs = 2000000;
+constexpr uint64_t kSvcWaitMutedNs = 20000000; // the test build's muted requests
 
 // Test hook, compiled into the test build only (librpccrc_test.so):
 // RPCCRC_TEST_SVC_MUTE=K makes the next K inline service requests unanswerable
-// (their tag never matches) and their wait 20 ms, to exercise the fallback.
+// (their tag never matches) and their first wait 20 ms, to exercise the fallback.
 bool take_test_svc_mute() {
 #ifdef RPCCRC_TEST_HOOKS
   static std::atomic<long> left{[] {
@@ -1095,23 +1106,52 @@ bool take_test_svc_mute() {
   return false;
 #endif
 }
-std::atomic<uint64_t> g_svc_fallbacks{0}; // calls that gave their service request up
 
 std::vector<Service *> g_services; // for the exit handler (under g_services_mu)
 std::mutex g_services_mu;
 
-// At process exit: ask every running instance to leave and wait (bounded) for
-// it, so no service wave outlives the process's last HIP call.
-void stop_services() {
-  std::lock_guard<std::mutex> g(g_services_mu);
-  for (Service *v : g_services) {
-    volatile uint32_t *ctl = v->sh->ctl;
-    ctl[kSvcStop] = 1u;
-    const uint64_t t0 = mono_ns();
-    while (ctl[kSvcExited] != v->launched && mono_ns() - t0 < 200000000ull) {
-    }
-  }
+bool svc_running(const Service &v) {
+  return *reinterpret_cast<const volatile uint32_t *>(&v.sh->ctl[kSvcExited]) !=
+         v.launched.load(std::memory_order_acquire);
 }
+
+// Asks every running instance to leave and waits for all of them together
+// (bounded: 200 ms), then clears the stop words so the next drop-in call's
+// instance serves as usual (unless `keep_stopped`, at exit).  g_services_mu is
+// held only to copy the list, and each launch_mu only to set / clear the word
+// (the waits no longer add up per device, and a first drop-in call
+// on another device does not block behind them).
+int svc_stop_list(bool keep_stopped) {
+  std::vector<Service *> vs;
+  {
+    std::lock_guard<std::mutex> g(g_services_mu);
+    vs = g_services;
+  }
+  std::vector<Service *> told;
+  for (Service *v : vs) {
+    std::lock_guard<std::mutex> lg(v->launch_mu);
+    if (!svc_running(*v)) continue;
+    reinterpret_cast<volatile uint32_t *>(v->sh->ctl)[kSvcStop] = 1u;
+    told.push_back(v);
+  }
+  const uint64_t t0 = mono_ns();
+  bool left = false;
+  while (!left && mono_ns() - t0 < 200000000ull) {
+    left = true;
+    for (Service *v : told) left = left && !svc_running(*v);
+  }
+  int rc = RPCCRC_OK;
+  for (Service *v : told) {
+    std::lock_guard<std::mutex> lg(v->launch_mu);
+    if (svc_running(*v)) rc = RPCCRC_EIO;
+    if (!keep_stopped) reinterpret_cast<volatile uint32_t *>(v->sh->ctl)[kSvcStop] = 0u;
+  }
+  return rc;
+}
+
+// At process exit: every running instance leaves, so no service wave outlives
+// the process's last HIP call.
+void stop_services() { (void)svc_stop_list(true); }
 
 void svc_init(DeviceCtx &c) {
   Service *v = new Service();
@@ -1140,29 +1180,8 @@ void svc_init(DeviceCtx &c) {
   c.svc = v;
 }
 
-bool svc_running(const Service &v) {
-  return *reinterpret_cast<const volatile uint32_t *>(&v.sh->ctl[kSvcExited]) !=
-         v.launched.load(std::memory_order_acquire);
-}
-
-// rpc_crc32_service_stop: the running instances leave now; the stop word is
-// cleared again so the next drop-in call's instance serves as usual.
-int svc_stop_all() {
-  std::lock_guard<std::mutex> g(g_services_mu);
-  int rc = RPCCRC_OK;
-  for (Service *v : g_services) {
-    std::lock_guard<std::mutex> lg(v->launch_mu); // no instance starts meanwhile
-    if (!svc_running(*v)) continue;
-    volatile uint32_t *ctl = v->sh->ctl;
-    ctl[kSvcStop] = 1u;
-    const uint64_t t0 = mono_ns();
-    while (svc_running(*v) && mono_ns() - t0 < 200000000ull) {
-    }
-    if (svc_running(*v)) rc = RPCCRC_EIO;
-    ctl[kSvcStop] = 0u;
-  }
-  return rc;
-}
+// rpc_crc32_service_stop: the running instances leave now.
+int svc_stop_all() { return svc_stop_list(false); }
 
 // Launches an instance unless one is running (the new one queues behind a
 // leaving one on the service stream).
@@ -1182,12 +1201,22 @@ bool svc_ensure(DeviceCtx &c, Service &v) {
 }
 
 // One drop-in CRC through the service; false when the service is off, busy
-// (every slot held) or failed to launch -- the caller then launches a kernel.
+// (every slot held), failed to launch, or gave the request up -- the caller then
+// launches a kernel.
 bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
   if (!service_enabled() || len > kSvcMaxLen) return false;
   std::call_once(c.svc_once, svc_init, std::ref(c));
   Service &v = *c.svc;
   if (!v.ok) return false;
+  SvcShared *sh = v.sh;
+  // After a request went unanswered: while the latest instance has not started
+  // (queued behind kernels that fill the GPU), take the launch path at once.
+  const bool degraded = v.degraded.load(std::memory_order_relaxed);
+  if (degraded && *reinterpret_cast<const volatile uint32_t *>(&sh->ctl[kSvcStarted]) !=
+                      v.launched.load(std::memory_order_acquire)) {
+    v.bypassed.fetch_add(1, std::memory_order_relaxed);
+    return false;
+  }
   // claim a slot: this thread's last one if free, else the lowest free one
   thread_local int last_slot = -1;
   int slot = -1;
@@ -1201,24 +1230,28 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
     }
   }
   last_slot = slot;
-  SvcShared *sh = v.sh;
   SvcReq &rq = sh->rq[slot];
   uint32_t q = ++v.seq[slot];
   if (q == 0) q = ++v.seq[slot]; // 0: the answered seq of a fresh slot
   const bool mute = len <= kSvcInline && take_test_svc_mute();
-  const uint64_t wait_ns = mute ? 20000000ull : kSvcWaitNs;
-  if (len <= kSvcInline) { // in the request block, ending at its inline byte 116; then line 1's tag
+  const uint64_t wait_ns = degraded ? kSvcWaitShortNs : mute ? kSvcWaitMutedNs : kSvcWaitNs;
+  // the tag: the check sum of the block's len, seq and inline words (the
+  // request's new bytes written into the shadow first), and of a longer body's
+  // masked words (crc32_kernels.h SvcReq)
+  uint32_t tag;
+  if (len <= kSvcInline) { // in the request block, ending at its inline byte 116
     uint8_t *shadow = reinterpret_cast<uint8_t *>(v.inl[slot]);
     memcpy(shadow + kSvcInline - len, src, len);
     memcpy(rq.inl + kSvcInline - len, src, len);
-    std::atomic_thread_fence(std::memory_order_release);
-    const uint32_t tag = svc_tag(len, q, v.inl[slot]);
-    *reinterpret_cast<volatile uint32_t *>(&rq.tag) = mute ? tag ^ 0x80000000u : tag;
+    tag = svc::block_sum(len, q, v.inl[slot]);
   } else {
     const uint32_t seg = svc::seg_of(len);
     memcpy(sh->body[slot] + 64u * seg - len, src, len);
+    tag = svc::block_sum(len, q, v.inl[slot]) ^ svc::body_sum(src, len);
   }
-  std::atomic_thread_fence(std::memory_order_release); // the body before the request word (x86: a compiler barrier)
+  std::atomic_thread_fence(std::memory_order_release); // the bytes before the tag (x86: a compiler barrier)
+  *reinterpret_cast<volatile uint32_t *>(&rq.tag) = mute ? tag ^ 0x80000000u : tag;
+  std::atomic_thread_fence(std::memory_order_release); // the tag before the request word
   *reinterpret_cast<volatile uint64_t *>(&rq.req) = (uint64_t)len | ((uint64_t)q << 32);
   bool ok = svc_ensure(c, v);
   const volatile uint64_t *res = &sh->res[slot][0];
@@ -1234,8 +1267,9 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
           ok = false;
           break;
         }
-        if ((spin & 4095u) == 0 && mono_ns() - t0 > wait_ns) { // give the request up (above)
-          g_svc_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        if ((spin & 1023u) == 0 && mono_ns() - t0 > wait_ns) { // give the request up (above)
+          (degraded ? v.fallbacks_short : v.fallbacks_full).fetch_add(1, std::memory_order_relaxed);
+          v.degraded.store(true, std::memory_order_relaxed);
           ok = false;
           break;
         }
@@ -1243,7 +1277,11 @@ bool svc_crc(DeviceCtx &c, const uint8_t *src, uint32_t len, uint32_t *crc) {
     }
   }
   v.busy.fetch_and(~(1u << slot), std::memory_order_release);
-  if (ok) *crc = (uint32_t)r;
+  if (ok) {
+    *crc = (uint32_t)r;
+    v.answered.fetch_add(1, std::memory_order_relaxed);
+    if (degraded) v.degraded.store(false, std::memory_order_relaxed);
+  }
   return ok;
 }
 
@@ -1636,6 +1674,26 @@ int rpc_crc32_device_status(void) {
 }
 
 int rpc_crc32_service_stop(void) { return svc_stop_all(); }
+
+int rpc_crc32_service_stats(rpccrc_service_stats_t *out) {
+  if (!out) return RPCCRC_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::vector<Service *> vs;
+  {
+    std::lock_guard<std::mutex> g(g_services_mu);
+    vs = g_services;
+  }
+  for (Service *v : vs) {
+    out->services += 1;
+    out->running += svc_running(*v) ? 1 : 0;
+    out->launched += v->launched.load(std::memory_order_acquire);
+    out->answered += v->answered.load(std::memory_order_relaxed);
+    out->fallbacks_full += v->fallbacks_full.load(std::memory_order_relaxed);
+    out->fallbacks_short += v->fallbacks_short.load(std::memory_order_relaxed);
+    out->bypassed += v->bypassed.load(std::memory_order_relaxed);
+  }
+  return RPCCRC_OK;
+}
 
 int rpc_crc32_device_clear_status(void) {
   DeviceCtx *c = nullptr;

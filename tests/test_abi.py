@@ -117,3 +117,12 @@ def test_test_library_exports_the_same_abi():
     assert sorted(line.split()[-1] for line in out.splitlines() if line.strip()) == header_symbols()
     assert b"RPCCRC_TEST_STEAL_GIVEUP" in open(test_lib, "rb").read()
     assert b"RPCCRC_TEST_STEAL_GIVEUP" not in open(LIB, "rb").read()
+
+
+def test_service_stats_without_a_service():
+    """rpc_crc32_service_stats before any drop-in call (no device needed): every
+    counter zero."""
+    import rpc_amd
+    st = rpc_amd.service_stats()
+    assert st == {k: 0 for k in ("services", "running", "launched", "answered", "fallbacks_full",
+                                 "fallbacks_short", "bypassed")}, st

@@ -106,3 +106,26 @@ def test_service_lane_algebra_matches_zlib(tmp_path):
     for k, (ln, got) in enumerate(zip(lens, out)):
         body = bytes(_mix(0x5E17C0DE + k * 4096 + i) & 0xFF for i in range(ln))
         assert int(got, 16) == zlib.crc32(body), ln
+
+
+def test_service_request_check_rejects_torn_reads(tmp_path):
+    """the drop-in service's request check (round 6:
+    crc32_service_math.h word_hash sums over the block and, for bodies over 116 B,
+    the body's masked words) rejects every mixed stale/current read of consecutive
+    JSON-RPC requests on one slot -- pairs of one length whose id and first parameter
+    step together (equal XOR deltas in two dwords), inline and body-area pairs
+    alternating; every subset of the changed words up to 2^14 reads per request,
+    seeded draws beyond.  The same enumeration under round 5's rule (a plain XOR of
+    the block, no check over 116 B) finds false accepts of both kinds, so the model
+    sees the bug class it is meant to exclude (tests/cpu_emu/svc_check_emu.cpp)."""
+    exe = str(tmp_path / "svc_check_emu")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(REPO, "tests/cpu_emu/svc_check_emu.cpp")],
+                   check=True)
+    r = subprocess.run([exe, "400"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = dict((k, int(v)) for k, v in (ln.split() for ln in r.stdout.splitlines()))
+    assert got["crosschecked"] > 10000
+    assert got["r6_reads"] > 1_000_000
+    assert got["r6_false_accepts"] == 0
+    assert got["r5_inline_false_accepts"] > 0
+    assert got["r5_false_accepts"] > got["r5_inline_false_accepts"]
