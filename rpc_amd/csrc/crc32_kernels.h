@@ -60,7 +60,69 @@ struct ItemsArgs {
   // Test-only (RPCCRC_TEST_STEAL_GIVEUP=1 in the environment): every pool-round
   // wait gives up at once, so the error path can be exercised deliberately.
   uint32_t test_giveup = 0;
+  // Dense span mode (crc32_rows.h kRowsSpanBnd): the span pass
+  // reads its stream base and length from span_ctl (the plan's output), each
+  // block's boundary record from span_rec, and stores per-boundary values into
+  // span_bnd.  nullptr: not a span pass.
+  const struct DenseCtl *span_ctl = nullptr;
+  const uint4 *span_rec = nullptr;
+  const uint16_t *span_bpos = nullptr;
+  uint4 *span_bnd = nullptr;
+  // Non-zero *skip_dev: the launch exits at once (the ragged rows pass of a
+  // batch the dense plan took; decided on the device).
+  const uint32_t *skip_dev = nullptr;
 };
+
+// ---- dense span mode -----------------------------------------
+// A ragged device batch whose bodies lie back to back in order, each of
+// kDenseMinBody .. kDenseMaxBody bytes (C2's layout), is CRC'd as ONE uniform
+// stream of 4 KiB blocks (the north star's kernel and rate) plus per-boundary
+// values, then folded per body -- instead of one wave walking each body's own
+// end-aligned rows (C2: 12.47M row steps against 9.66M blocks).  Decided on the
+// device by dense_plan_kernel; a batch that is not dense runs the rows pass.
+constexpr uint32_t kDenseMinBody = 64;          // at most one boundary per 64-B segment of a block
+constexpr uint32_t kDenseMaxBody = 1u << 20;    // the fold's thread-per-body Horner (<= 257 blocks)
+constexpr uint64_t kDenseMinN = 1u << 16;       // smaller batches stay on the rows path
+constexpr uint64_t kDenseMaxN = (1u << 25) - 2; // boundary indices fit 25 bits of a block record
+constexpr uint64_t kDenseMaxBlocks = 1ull << 24; // 64 GiB of stream per call
+constexpr uint32_t kDenseInline = 6;            // boundary offsets carried in a block record
+// Plan output (device).  nblocks = 0: the batch is not dense (the rows pass
+// runs; the span and fold passes exit at once).
+struct DenseCtl {
+  uint64_t anchor;  // stream base: the first body's address rounded down to 16 B
+  uint64_t bytes;   // anchor .. the last body's end
+  uint64_t nblocks; // 4 KiB blocks of the stream (the span pass's device count)
+  uint32_t skip;    // 1 when dense: the rows pass exits at once
+  uint32_t pad;
+};
+// Block record (every block of the stream): x = first boundary index in the
+// block | count << 25; y, z, w = the block offsets (12 bits, as u16) of its
+// first kDenseInline boundaries.
+// Boundary g (body g's start; g = n: the last body's end) at stream offset
+// rel_g: bpos[g] = rel_g & 4095.  Span pass output per boundary:
+// bnd[g] = {P1, cap, Qp, block} (tests/test_dense_emu.py names them).
+struct DenseArgs {
+  const uint8_t *base;
+  const uint64_t *offsets;
+  const uint32_t *lengths;
+  uint64_t n;
+  uint64_t nb_cap;    // records / W words in the workspace
+  DenseCtl *ctl;
+  uint4 *rec;         // nb_cap
+  uint16_t *bpos;     // n + 1
+  uint4 *bnd;         // n + 1
+  uint32_t *W;        // nb_cap: crc0 of each block (the span pass's out)
+  uint32_t *flags;    // dense_plan_blocks(n): the plan's per-workgroup "not dense" flags
+  uint32_t *out;      // n CRCs
+  const uint32_t *tq; // Tq[q] = A_q(0xFFFFFFFF)
+  const uint32_t *tab; // kDenseTabWords: the fold's maps (crc32_layout.h)
+};
+size_t dense_workspace_bytes(uint64_t n, uint64_t nb_cap);
+DenseArgs dense_carve(void *ws, uint64_t n, uint64_t nb_cap);
+inline uint64_t dense_plan_blocks(uint64_t n) { return (n + 1 + 255) / 256; } // 4 waves of 64 boundaries each
+// The plan (dense_plan_kernel) and the decision (dense_decide_kernel: DenseCtl).
+hipError_t launch_dense_plan(const DenseArgs &d, hipStream_t s);
+hipError_t launch_dense_fold(const DenseArgs &d, int cus, hipStream_t s);
 
 constexpr uint32_t kStealOnDevice = 0xFFFFFFFFu; // ItemsArgs.steal_s: computed in the kernel (device-counted n)
 

@@ -331,6 +331,26 @@ hipError_t launch_rows(const ItemsArgs &a, int QB, bool nt, int max_blocks, hipS
     k.steal_s = kStealOnDevice; // device-counted: the kernel sizes the pool from *n_dev
   }
   if (k.steal_s == 0) k.steal = nullptr;
+  if (a.span_ctl != nullptr) { // kRowsSpanBnd: the dense span pass (DYN, 4096-byte uniform RAW items, device count)
+    if (QB != 1 || ragged || !dyn || a.len != 4096 || a.stride != 4096 || a.mode != kModeRaw || a.n_dev == nullptr ||
+        a.out_idx != nullptr || a.span_rec == nullptr || a.span_bnd == nullptr || a.span_bpos == nullptr)
+      return hipErrorInvalidValue;
+#define RPCCRC_ROWS_SPAN(N)                                                                                       \
+  do {                                                                                                            \
+    if (k.steal_s && steal_done) {                                                                                \
+      hipExtLaunchKernelGGL((crc32_rows_kernel<1, N, false, kRowsSpanBnd, 1, true, true>), grid, block, 0, stream, \
+                            nullptr, steal_done, 0, k);                                                           \
+      if (steal_recorded) *steal_recorded = true;                                                                 \
+    } else if (k.steal_s) {                                                                                       \
+      hipLaunchKernelGGL((crc32_rows_kernel<1, N, false, kRowsSpanBnd, 1, true, true>), grid, block, 0, stream, k); \
+    } else {                                                                                                      \
+      hipLaunchKernelGGL((crc32_rows_kernel<1, N, false, kRowsSpanBnd, 1, true>), grid, block, 0, stream, k);    \
+    }                                                                                                             \
+  } while (0)
+    if (nt) RPCCRC_ROWS_SPAN(true); else RPCCRC_ROWS_SPAN(false);
+#undef RPCCRC_ROWS_SPAN
+    return hipGetLastError();
+  }
   if (a.round_out != nullptr) { // kRowsRoundOut: whole DYN rounds of 4096-byte uniform RAW items
     if (QB != 1 || ragged || !dyn || a.len != 4096 || a.stride != 4096 || a.mode != kModeRaw ||
         a.out_idx != nullptr || (reinterpret_cast<uintptr_t>(a.base) & 15u) != 0)
@@ -1405,6 +1425,292 @@ hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool 
     else
       hipLaunchKernelGGL((stream_read_kernel<1, false>), grid, block, 0, stream, q, ntiles, out);
   }
+  return hipGetLastError();
+}
+
+// ---- dense span mode (tests/test_dense_emu.py restates it) ----
+
+size_t dense_workspace_bytes(uint64_t n, uint64_t nb_cap) {
+  return align256(sizeof(DenseCtl)) + align256(nb_cap * 16) + align256((n + 1) * 2) + align256((n + 1) * 16) +
+         align256(nb_cap * 4) + align256(dense_plan_blocks(n) * 4);
+}
+
+DenseArgs dense_carve(void *ws, uint64_t n, uint64_t nb_cap) {
+  uint8_t *w = static_cast<uint8_t *>(ws);
+  auto take = [&](size_t bytes) {
+    uint8_t *p = w;
+    w += align256(bytes);
+    return p;
+  };
+  DenseArgs d{};
+  d.n = n;
+  d.nb_cap = nb_cap;
+  d.ctl = reinterpret_cast<DenseCtl *>(take(sizeof(DenseCtl)));
+  d.rec = reinterpret_cast<uint4 *>(take(nb_cap * 16));
+  d.bpos = reinterpret_cast<uint16_t *>(take((n + 1) * 2));
+  d.bnd = reinterpret_cast<uint4 *>(take((n + 1) * 16));
+  d.W = reinterpret_cast<uint32_t *>(take(nb_cap * 4));
+  d.flags = reinterpret_cast<uint32_t *>(take(dense_plan_blocks(n) * 4));
+  return d;
+}
+
+namespace {
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t ballot64(bool p) { return (uint64_t)__builtin_amdgcn_ballot_w64(p); }
+
+// Decides whether the batch is dense -- every body kDenseMinBody ..
+// kDenseMaxBody bytes and starting where the previous one ends -- and writes
+// the span pass's inputs: per boundary its block offset (bpos), per block its
+// record (first boundary, count, the first kDenseInline offsets; a block
+// without a boundary: count 0).  One wave per window of 64 boundaries g0 ..
+// g0 + 63 (lane L: boundary g0 + L), all its loads issued at once (loads under
+// per-lane branches had each waited out its own round trip: 190 us for C2);
+// it looks at the next window too (a block holds at most 64 boundaries, so a
+// run that starts in the window ends before the next window's end).  The
+// first boundary of each block writes its record, and the records of the
+// empty blocks before it (inside the previous body) are dealt over the wave's
+// lanes.  Each workgroup stores whether it found the batch not dense
+// (dense_decide_kernel reads them).
+__global__ __launch_bounds__(256) void dense_plan_kernel(DenseArgs d) {
+  const uint64_t n = d.n;
+  const uint64_t base = (uint64_t)(uintptr_t)d.base;
+  const uint64_t anchor = (base + d.offsets[0]) & ~(uint64_t)15;
+  const uint64_t rel_n = base + d.offsets[n - 1] + d.lengths[n - 1] - anchor;
+  const uint64_t nblocks = (rel_n + 4095u) >> 12;
+  constexpr uint64_t kNone = ~(uint64_t)0; // past boundary n: a block of its own
+  bool bad = nblocks > d.nb_cap || nblocks > kDenseMaxBlocks;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);
+  const uint64_t g0 = 64u * w, g = g0 + lane;
+  if (g0 <= n) { // (wave-uniform)
+    // every load at once, indices clamped; selects after
+    const uint64_t oa = d.offsets[min(g, n - 1)], ob = d.offsets[min(g + 64u, n - 1)];
+    const uint32_t L = d.lengths[min(g, n - 1)];
+    const uint64_t op = d.offsets[g0 == 0 ? 0 : g0 - 1]; // (lane 0's previous boundary)
+    const bool va = g <= n;
+    const uint64_t ra = g < n ? base + oa - anchor : (g == n ? rel_n : kNone);
+    const uint64_t rb = g + 64u < n ? base + ob - anchor : (g + 64u == n ? rel_n : kNone); // the next window
+    uint64_t rp = shfl64(ra, (int)((lane + 63u) & 63u)); // the previous boundary
+    if (lane == 0u) rp = g0 == 0 ? 0u : base + op - anchor;
+    const uint64_t rn_b = shfl64(rb, 0);
+    uint64_t rn = shfl64(ra, (int)((lane + 1u) & 63u)); // the next boundary
+    if (lane == 63u) rn = rn_b;
+    if (g < n && (L < kDenseMinBody || L > kDenseMaxBody || rn - ra != L)) bad = true;
+    if (va) d.bpos[g] = (uint16_t)(ra & 4095u);
+    const uint64_t ja = ra >> 12, jp = rp >> 12, jb = rb >> 12;
+    const bool first = g == 0 || ja != jp; // (the first lane past boundary n counts as one: it ends the run)
+    if (va && g != 0 && ja != jp && (ja < jp || ja - jp > (kDenseMaxBody >> 12) + 2)) bad = true; // out of order
+    // boundaries of this lane's block from this lane on: to the next first lane,
+    // else through lane 63 and on into the next window
+    const uint64_t F = ballot64(first);
+    const uint64_t ja63 = shfl64(ja, 63);
+    const uint64_t B = ballot64(jb != ja63);
+    const uint64_t after = lane == 63u ? 0u : F >> (lane + 1u);
+    const uint32_t cnt = after ? (uint32_t)__builtin_ctzll(after) + 1u
+                               : 64u - lane + (B ? (uint32_t)__builtin_ctzll(B) : 64u);
+    if (va && first && cnt > 64u) bad = true; // (bodies under 64 B: caught above as well)
+    uint32_t o[kDenseInline];
+#pragma unroll
+    for (uint32_t i = 0; i < kDenseInline; ++i) {
+      const uint32_t src = lane + i;
+      const uint32_t qa = (uint32_t)__shfl((int)(uint32_t)(ra & 4095u), (int)(src & 63u), 64);
+      const uint32_t qb = (uint32_t)__shfl((int)(uint32_t)(rb & 4095u), (int)(src & 63u), 64);
+      o[i] = i < cnt ? (src < 64u ? qa : qb) : 0u;
+    }
+    if (va && first && ja < nblocks)
+      d.rec[ja] = make_uint4((uint32_t)g | (min(cnt, 64u) << 25), o[0] | (o[1] << 16), o[2] | (o[3] << 16),
+                             o[4] | (o[5] << 16));
+    // empty blocks (jp, ja) before a first boundary: k records, dealt over the wave
+    uint32_t k = 0;
+    if (va && first && g != 0 && ja > jp + 1u && ja - jp <= (kDenseMaxBody >> 12) + 2)
+      k = (uint32_t)(min(ja, nblocks) > jp + 1u ? min(ja, nblocks) - jp - 1u : 0u);
+    uint32_t incl = k;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)incl, dd, 64);
+      if ((int)lane >= dd) incl += t;
+    }
+    const uint32_t K = (uint32_t)__shfl((int)incl, 63, 64);
+    for (uint32_t q0 = 0; q0 < K; q0 += 64u) {
+      const uint32_t q = q0 + lane;
+      uint32_t own = 0; // the first lane whose inclusive sum passes q
+#pragma unroll
+      for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)incl, (int)(own + step - 1u), 64);
+        if (v <= q) own += step;
+      }
+      own = min(own, 63u);
+      const uint64_t jp_o = shfl64(jp, (int)own);
+      const uint32_t ex_o = (uint32_t)__shfl((int)(incl - k), (int)own, 64);
+      const uint64_t j = jp_o + 1u + (q - ex_o);
+      if (q < K && j < nblocks) d.rec[j] = make_uint4((uint32_t)(g0 + own), 0u, 0u, 0u);
+    }
+  }
+  const int any_bad = __syncthreads_or(bad ? 1 : 0);
+  if (threadIdx.x == 0) d.flags[blockIdx.x] = any_bad ? 1u : 0u; // (every word written: no clearing)
+}
+
+// One workgroup: ORs the plan's per-workgroup flags and writes DenseCtl
+// (nblocks = 0 unless dense).  (The plan's workgroups had each counted
+// themselves done on one device atomic, 16K of them: 1.4 ms.)
+__global__ __launch_bounds__(1024) void dense_decide_kernel(DenseArgs d, uint32_t plan_blocks) {
+  uint32_t bad = 0;
+  for (uint32_t i = threadIdx.x; i < plan_blocks; i += 1024u) bad |= d.flags[i];
+  bad = __syncthreads_or((int)bad);
+  if (threadIdx.x == 0) {
+    const uint64_t n = d.n;
+    const uint64_t base = (uint64_t)(uintptr_t)d.base;
+    const uint64_t anchor = (base + d.offsets[0]) & ~(uint64_t)15;
+    const uint64_t rel_n = base + d.offsets[n - 1] + d.lengths[n - 1] - anchor;
+    const uint64_t nblocks = (rel_n + 4095u) >> 12;
+    const bool dense = bad == 0u && nblocks <= d.nb_cap && nblocks <= kDenseMaxBlocks && n >= 1 && n <= kDenseMaxN;
+    d.ctl->anchor = anchor;
+    d.ctl->bytes = rel_n;
+    d.ctl->nblocks = dense ? nblocks : 0u;
+    d.ctl->skip = dense ? 1u : 0u;
+  }
+}
+
+// Nibble map `map` of x from the LDS copy of the maps (crc32_layout.h
+// kDenseTabWords: word (n * 16 + nib) * kDenseMaps + map).
+__device__ __forceinline__ uint32_t dense_map(const uint32_t *t, uint32_t map, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) r ^= t[(k * 16u + ((x >> (4u * k)) & 15u)) * kDenseMaps + map];
+  return r;
+}
+
+// Per boundary g: E = crc0(its block with the bytes from g on zeroed)
+//   = A_{1024(3-hi)}(P1 ^ A_{4(256 - 16 lo - tb)}(cap)) ^ Qp.
+// Per body g over blocks j .. j1 (D = j1 - j):
+//   j1 = j:  Y = Tq[4096 - off] ^ E(g) ^ E_end
+//   j1 > j:  Y = A_{4096 D}(Tq[4096 - off] ^ W[j] ^ E(g)) ^ X ^ E_end,
+//            X = XOR over the blocks i in between of A_{4096 (j1 - i)}(W[i])
+// with E_end = E(g + 1), or W[j1] when the body ends its block; then
+// crc = ~A_{-z}(Y), z = 4096 - e_off (the bytes of j1 after the body).  A wave
+// takes boundaries 63 w .. 63 w + 63 and bodies 63 w .. 63 w + 62 (body g's
+// end boundary is lane g + 1's); the in-between blocks of its bodies are dealt
+// over its lanes (one block each per pass, XORed into an LDS word per body),
+// so a long body does not hold the wave for a Horner step per block.
+__global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
+  __shared__ uint32_t s_tab[kDenseTabWords];
+  __shared__ uint32_t s_x[16 * 64];
+  if (d.ctl->nblocks == 0u) return; // (block-uniform) not dense: the rows pass did it
+  for (uint32_t i = threadIdx.x; i < kDenseTabWords; i += 1024u) s_tab[i] = d.tab[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t *x_acc = s_x + wave * 64u;
+  const uint64_t n = d.n, nw = (n + 62) / 63, last_w = d.nb_cap - 1;
+  const uint64_t base = (uint64_t)(uintptr_t)d.base, anchor = d.ctl->anchor, rel_n = d.ctl->bytes;
+  for (uint64_t w = (uint64_t)blockIdx.x * 16u + wave; w < nw; w += (uint64_t)gridDim.x * 16u) {
+    const uint64_t g = 63u * w + lane;
+    // round trip 1: boundary g's offset and values, body g's length (every
+    // index clamped, no load under a branch)
+    const uint64_t o = d.offsets[min(g, n - 1)];
+    const uint32_t L = d.lengths[min(g, n - 1)];
+    const uint4 b = d.bnd[min(g, n)];
+    const bool body = lane < 63u && g < n;
+    const uint64_t rs = g < n ? base + o - anchor : rel_n; // stream offset of boundary g
+    const uint64_t j = rs >> 12;
+    const uint32_t off = (uint32_t)(rs & 4095u);
+    const uint64_t re = rs + L; // body g's end
+    const uint64_t j1 = (re - 1) >> 12;
+    const uint32_t e_off = (uint32_t)(re - j1 * 4096u); // 1 .. 4096
+    // the blocks in between: m per body, dealt over the wave's lanes
+    const uint32_t m = (body && j1 > j + 1u) ? (uint32_t)(j1 - j - 1u) : 0u;
+    uint32_t incl = m;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)incl, dd, 64);
+      if ((int)lane >= dd) incl += t;
+    }
+    const uint32_t K = (uint32_t)__shfl((int)incl, 63, 64);
+    // lane q's in-between block for pass q0: its body (owner), index and distance
+    auto deal = [&](uint32_t q0, uint64_t &i, uint32_t &dist, uint32_t &own) {
+      const uint32_t q = q0 + lane;
+      own = 0; // the first lane whose inclusive sum passes q
+#pragma unroll
+      for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)incl, (int)(own + step - 1u), 64);
+        if (v <= q) own += step;
+      }
+      own = min(own, 63u);
+      const uint64_t jo = shfl64(j, (int)own), j1o = shfl64(j1, (int)own);
+      const uint32_t exo = (uint32_t)__shfl((int)(incl - m), (int)own, 64);
+      i = q < K ? jo + 1u + (q - exo) : 0u;
+      dist = q < K ? (uint32_t)(j1o - i) : 0u; // 1 .. 256
+    };
+    uint64_t i0;
+    uint32_t dist0, own0;
+    deal(0u, i0, dist0, own0);
+    // round trip 2: seed, first / last block CRCs, the first pass's blocks
+    const uint32_t tqv = d.tq[4096u - off];
+    const uint32_t wj = d.W[body ? min(j, last_w) : 0u];
+    const uint32_t wj1 = d.W[body ? min(j1, last_w) : 0u];
+    const uint32_t wi0 = d.W[min(i0, last_w)];
+    x_acc[lane] = 0u;
+    const uint32_t k = off >> 6, hi = k >> 4, lo = k & 15u, tb = (off & 63u) >> 2;
+    const uint32_t n1 = 256u - 16u * lo - tb; // 1 .. 256
+    uint32_t y = dense_map(s_tab, kDenseM4 + (n1 & 15u), b.y);
+    y = dense_map(s_tab, kDenseM64 + (n1 >> 4), y);
+    const uint32_t E = dense_map(s_tab, kDenseMQ + (3u - hi), b.x ^ y) ^ b.z;
+    const uint32_t En = (uint32_t)__shfl_down((int)E, 1, 64);
+    if (lane < K) {
+      uint32_t c = dense_map(s_tab, kDenseMB0 + (dist0 & 15u), wi0);
+      c = dense_map(s_tab, kDenseMB1 + (dist0 >> 4), c);
+      __hip_atomic_fetch_xor(&x_acc[own0], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    for (uint32_t q0 = 64u; q0 < K; q0 += 64u) { // (long bodies)
+      uint64_t i;
+      uint32_t dist, own;
+      deal(q0, i, dist, own);
+      const uint32_t wi = d.W[min(i, last_w)];
+      if (q0 + lane < K) {
+        uint32_t c = dense_map(s_tab, kDenseMB0 + (dist & 15u), wi);
+        c = dense_map(s_tab, kDenseMB1 + (dist >> 4), c);
+        __hip_atomic_fetch_xor(&x_acc[own], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      }
+    }
+    const uint32_t X = x_acc[lane];
+    if (body) {
+      const uint32_t Ee = e_off == 4096u ? wj1 : En;
+      uint32_t acc = tqv ^ E;
+      if (j1 == j) {
+        acc ^= Ee;
+      } else {
+        const uint32_t D = (uint32_t)(j1 - j); // 1 .. 257
+        acc = dense_map(s_tab, kDenseMB0 + (D & 15u), acc ^ wj);
+        acc = dense_map(s_tab, kDenseMB1 + (D >> 4), acc) ^ X ^ Ee;
+      }
+      const uint32_t z = 4096u - e_off;
+      acc = dense_map(s_tab, kDenseMI0 + (z & 15u), acc);
+      acc = dense_map(s_tab, kDenseMI1 + ((z >> 4) & 15u), acc);
+      acc = dense_map(s_tab, kDenseMI2 + (z >> 8), acc);
+      d.out[g] = ~acc;
+    }
+  }
+}
+
+} // namespace
+
+hipError_t launch_dense_plan(const DenseArgs &d, hipStream_t s) {
+  if (d.n == 0 || d.n > kDenseMaxN || d.flags == nullptr) return hipErrorInvalidValue;
+  const uint64_t blocks = dense_plan_blocks(d.n); // one wave per 64 boundaries
+  hipLaunchKernelGGL(dense_plan_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(dense_decide_kernel, dim3(1), dim3(1024), 0, s, d, (uint32_t)blocks);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_fold(const DenseArgs &d, int cus, hipStream_t s) {
+  const uint64_t nw = (d.n + 62) / 63;
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((nw + 15) / 16, 2ull * (uint64_t)std::max(cus, 1)));
+  hipLaunchKernelGGL(dense_fold_kernel, dim3((unsigned)blocks), dim3(1024), 0, s, d);
   return hipGetLastError();
 }
 

@@ -108,6 +108,17 @@ constexpr uint32_t kBigDbl = 11;          // i = 10: A_{1024 * chunk}, the Horne
 constexpr uint32_t kBigDblWords = kBigChunkClasses * kBigDbl * 128;
 void build_big_dbl(uint32_t *tab /* kBigDblWords */);
 
+// The dense span fold's maps (crc32_kernels.hip dense_fold_kernel, DESIGN.md
+// 4.9), stored [n][nib][map] (word (n * 16 + nib) * kDenseMaps + map: the
+// lanes of one lookup, each with its own map, spread over all 32 banks; a
+// [map][n][nib] layout put one lookup on 16 banks): A_{4b} (b = 0..15), A_{64a} (a = 0..16),
+// A_{1024h} (h = 0..3), A_{-z0}, A_{-16 z1}, A_{-256 z2} (0..15 each),
+// A_{4096 d0} (d0 = 0..15), A_{65536 d1} (d1 = 0..16).
+constexpr uint32_t kDenseM4 = 0, kDenseM64 = 16, kDenseMQ = 33, kDenseMI0 = 37, kDenseMI1 = 53, kDenseMI2 = 69,
+                   kDenseMB0 = 85, kDenseMB1 = 101, kDenseMaps = 118;
+constexpr uint32_t kDenseTabWords = kDenseMaps * 128;
+void build_dense_tab(uint32_t *tab /* kDenseTabWords */);
+
 // One-wave scalar kernel (crc32_scalar.hip): bodies of <= kScalarMaxLen
 // bytes.  Table image of kScalarTabWords words: T_k[256] slice-by-4 tables,
 // k = 0..3, then NIB[k - kScalarNibK0][i][j] = A_{2^k bytes}(j << 4i) for

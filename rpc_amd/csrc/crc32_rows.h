@@ -128,8 +128,8 @@ constexpr uint32_t kOobOffset = 0x7FFFFFF0u;
 static_assert(kOobOffset >= kRsrcRange, "the out-of-range offset must fail the range check");
 // Flags 0x00020000: DATA_FORMAT 32 (a descriptor with format 0, "invalid",
 // reads zeros).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(uint64_t base) {
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)kRsrcRange, 0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(uint64_t base, uint32_t range = kRsrcRange) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)range, 0x00020000);
 }
 // Cache-policy bits of the non-temporal row loads (the builtin's aux operand;
 // 2 = nt).  RPCCRC_ROW_AUX overrides them for A/B builds only: sc0|nt, sc1|nt
@@ -413,6 +413,13 @@ constexpr int kRowsAblPipeMem = 65536;
 // which such launches never read (16-byte aligned items of 4096 bytes have no
 // trailing pad; the host requires the aligned base).
 constexpr int kRowsRoundOut = 32768;
+// Feature bit (product): the dense span pass (ItemsArgs.span_*).
+// Uniform QB = 1 RAW rows over one stream of 4 KiB blocks (base and length
+// from the plan's DenseCtl, the last block range-checked at the stream's end);
+// a block whose record lists body boundaries also stores, per boundary, the
+// in-quarter prefix P1, the chain state cap at the boundary's dword and the
+// quarter prefix Qp (tests/test_dense_emu.py), from values the lanes hold.
+constexpr int kRowsSpanBnd = 131072;
 // QB = 1 software pipeline over rows (chain of row r+1 beside the merge of row r).
 #ifndef RPCCRC_ROWS_PIPE
 #define RPCCRC_ROWS_PIPE 1
@@ -614,6 +621,47 @@ __device__ __forceinline__ uint32_t nib_map_at(const uint8_t *lds, uint32_t s) {
     t[2 * k + 1] = lds_ld(lds, __builtin_amdgcn_perm(xh4, TAB, 0x0C020104u + k) + k * 128u + 64u);
   }
   return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// ---- dense span rows (kRowsSpanBnd) ----
+// The chain of seg_crc, also capturing cap = X_tb ^ (w_tb & nm): the state
+// after the boundary's dword tb (X_0 = w_0, X_t = A_4(X_{t-1}) ^ w_t) with the
+// dword's bytes at or after the boundary (nm) taken out again.  tb = 16 in
+// lanes without a boundary (cap stays 0).
+__device__ __forceinline__ uint32_t seg_crc_cap(const uint8_t *lds, const u32x4 (&p)[4], uint32_t lsel, uint32_t tb,
+                                                uint32_t nm, uint32_t &cap) {
+  uint32_t x = p[0][0];
+  uint32_t c = (tb == 0u) ? (x & ~nm) : 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (k == 0 && d == 0) continue;
+      x = slice4w(lds, x, p[k][d], lsel);
+      c = (tb == (uint32_t)(4 * k + d)) ? __builtin_amdgcn_bitop3_b32(p[k][d], nm, x, 0x6A) : c; // (w & nm) ^ x
+    }
+  cap = c;
+  return slice4(lds, x, lsel);
+}
+// Inclusive XOR scan over the 16 lanes of each DPP row (row_shr, zeros shifted in).
+__device__ __forceinline__ uint32_t row_xor_scan(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true); // row_shr:1
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xF, 0xF, true); // row_shr:2
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true); // row_shr:4
+  return v ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x118, 0xF, 0xF, true); // row_shr:8
+}
+// merge_row's distributed ST2 step without the cross-row XOR: the four
+// shifted quarter values Vs_h = A_{1024(3-h)}(v_h) as scalars (lane 16h + 4).
+struct RowQuarterVals {
+  uint32_t vs[4];
+};
+__device__ __forceinline__ RowQuarterVals merge_quarters(const uint8_t *lds, uint32_t v, const DistLane &d) {
+  const uint32_t nib = ((d.own ? v : 0u) >> d.shift) & 15u;
+  const uint32_t t = dist_reduce8(lds_ld(lds, d.row_base + nib * d.row_mul));
+  RowQuarterVals r;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) r.vs[h] = (uint32_t)__builtin_amdgcn_readlane((int)t, 16 * h + 4);
+  return r;
 }
 
 struct QuarterInfo {
@@ -822,6 +870,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   // before the 155 KiB image copy (block-uniform).
   if (blockIdx.x == 0 && threadIdx.x < a.zero_n) a.zero_out[threadIdx.x] = 0u;
   if (a.n_dev != nullptr && ld_const(a.n_dev, 0) == 0) return;
+  if (a.skip_dev != nullptr && ld_const(a.skip_dev, 0) != 0u) return; // (a dense batch: the span pass has it)
   uint64_t t_entry = 0, t_image = 0;
   if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   // All of this thread's image loads in flight at once (a rolled loop would
@@ -885,6 +934,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   const uint32_t gw = vb * 16u + wave;
   const uint32_t mode = a.mode;
   const uint32_t n = (uint32_t)(a.n_dev ? ld_const(a.n_dev, 0) : a.n_items);
+  // Dense span pass (kRowsSpanBnd): item j is block j of the plan's stream.
+  constexpr bool kSpan = (ABL & kRowsSpanBnd) != 0 && QB == 1 && !RAGGED;
+  const uint64_t span_base = kSpan ? ld_const(reinterpret_cast<const uint64_t *>(a.span_ctl), 0) : 0u;
+  const uint64_t span_end = kSpan ? span_base + ld_const(reinterpret_cast<const uint64_t *>(a.span_ctl), 1) : 0u;
   auto oidx = [&](uint32_t i) -> uint32_t { return a.out_idx ? a.out_idx[i] : i; }; // output slot
   auto store_out = [&](uint32_t *p, uint32_t v) {
     if constexpr ((ABL & kRowsAblNtStore) != 0) __builtin_nontemporal_store(v, p);
@@ -1110,6 +1163,15 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     // 0 can start before the item (when hd < 4096).
     auto meta = [&](uint32_t item, uint64_t &p0, uint32_t &hd, uint32_t &len, uint32_t &z, uint32_t &nr,
                     uint32_t &seed) {
+      if constexpr (kSpan) { // one 4 KiB block, no pad, RAW
+        p0 = span_base + (uint64_t)item * kRow;
+        len = kRow;
+        z = 0u;
+        nr = 1u;
+        hd = kRow;
+        seed = 0u;
+        return;
+      }
       uint64_t off = RAGGED ? ld_const(a.offsets, item) : (uint64_t)item * a.stride;
       len = RAGGED ? ld_const(a.lengths, item) : a.len;
       if constexpr (RAGGED && kMetaCoissue) __asm__ volatile("" : "+s"(off), "+s"(len)); // both loads, one wait
@@ -1160,7 +1222,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           for (int b = 0; b < 4; ++b) // negative offsets (pieces before the item) -> kOobOffset: one v_min_u32
             off[b] = min((uint32_t)(d + (int32_t)(pofs + b * kQuarter)), kOobOffset);
         }
-        const __amdgpu_buffer_rsrc_t row = row_rsrc(base);
+        // (span pass: the stream's last block reads zeros past its end, rounded
+        // up to 16 B -- inside the 16-B block holding the last body byte)
+        const uint64_t rem = span_end - base;
+        const __amdgpu_buffer_rsrc_t row =
+            row_rsrc(base, (kSpan && rem < kRow) ? (uint32_t)((rem + 15u) & ~(uint64_t)15) : kRsrcRange);
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           // RPCCRC_RAGGED_Q3_TEMPORAL (A/B): a ragged row's last quarter through
@@ -1311,6 +1377,84 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         m.rwu = W;
       }
       finish(valid, len, z, nr, r, seed, cidx, tsk, m);
+    };
+
+    // ---- dense span pass (kSpan) ----
+    // Block j's record {first | cnt << 25, offsets of its first kDenseInline
+    // boundaries} comes with the block's row loads as a VECTOR load (one 16-B
+    // request, every lane the same address): a scalar load in flight would make
+    // each chain step's LDS wait an lgkmcnt(0) (SMEM returns out of order).
+    // (A separate count array, one byte a block, measured the span pass +3.4 %
+    // for the second load per row: profiles/r06d.)
+    auto span_record = [&](uint32_t item) -> u32x4 {
+      const __amdgpu_buffer_rsrc_t rr = row_rsrc((uint64_t)(uintptr_t)a.span_rec);
+      return __builtin_amdgcn_raw_buffer_load_b128(rr, 0, (int)(item * 16u), 0);
+    };
+    // A block without boundaries: the plain row (W only).  With boundaries:
+    // lane k's segment holds at most one (bodies are >= 64 B); occ marks those
+    // segments and the boundary in segment k is the block's src-th, src = the
+    // bits of occ below k (mbcnt).  The chain also captures cap at the
+    // boundary's dword; P1 = the exclusive in-quarter XOR scan of the ST1-shifted
+    // segment CRCs; Qp = the XOR of the shifted quarters before this one.
+    auto compute_span = [&](bool valid, uint32_t cidx, uint32_t tsk, uint32_t item, u32x4 (&buf)[4],
+                            const u32x4 &recv) {
+      const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)recv[0]);
+      const uint32_t first = r0 & 0x1FFFFFFu, cnt = r0 >> 25;
+      transpose(buf);
+      RowMerge m;
+      m.rwu = 0u;
+      if (cnt == 0u || !valid) {
+        m.crc = merge_row(lds, merge_lo(lds, seg_crc(lds, buf, lsel), lsel1), 0u, dl).crc;
+      } else {
+        const uint32_t rw[3] = {(uint32_t)__builtin_amdgcn_readfirstlane((int)recv[1]),
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)recv[2]),
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)recv[3])};
+        uint64_t occ = 0;
+        uint32_t pos_l = 0; // > kDenseInline boundaries: lane L < cnt holds boundary L's block offset
+        if (cnt <= kDenseInline) {
+#pragma unroll
+          for (uint32_t i = 0; i < kDenseInline; ++i)
+            if (i < cnt) occ |= 1ull << (((rw[i >> 1] >> (16u * (i & 1u))) & 0xFFFu) >> 6);
+        } else {
+          pos_l = lane < cnt ? (uint32_t)a.span_bpos[first + lane] : 0u;
+          uint32_t ol = 0, oh = 0;
+          if (lane < cnt) {
+            const uint32_t k = pos_l >> 6;
+            ol = k < 32u ? 1u << k : 0u;
+            oh = k >= 32u ? 1u << (k - 32u) : 0u;
+          }
+#pragma unroll
+          for (int mm = 1; mm < 64; mm <<= 1) {
+            ol |= (uint32_t)__shfl_xor((int)ol, mm, 64);
+            oh |= (uint32_t)__shfl_xor((int)oh, mm, 64);
+          }
+          occ = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)oh) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((int)ol);
+        }
+        const bool has = ((occ >> lane) & 1u) != 0u;
+        const uint32_t src = __builtin_amdgcn_mbcnt_hi((uint32_t)(occ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)occ, 0u));
+        uint32_t pos;
+        if (cnt <= kDenseInline) {
+          const uint32_t w = src < 2u ? rw[0] : (src < 4u ? rw[1] : rw[2]);
+          pos = ((src & 1u) ? (w >> 16) : w) & 0xFFFu;
+        } else {
+          pos = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4u), (int)pos_l);
+        }
+        const uint32_t rr = pos & 63u;
+        uint32_t cap;
+        const uint32_t c = seg_crc_cap(lds, buf, lsel, has ? rr >> 2 : 16u, 0xFFFFFFFFu << (8u * (rr & 3u)), cap);
+        const uint32_t d1 = st1_map(lds, c, lsel1); // A_{64(15-lo)}
+        const uint32_t p1 = row_xor_scan(d1) ^ d1;  // exclusive in-quarter prefix
+        uint32_t v = d1 ^ dpp_xor1(d1);
+        v ^= dpp_xor2(v);
+        v ^= dpp_ror4(v);
+        v ^= dpp_ror8(v);
+        const RowQuarterVals q = merge_quarters(lds, v, dl);
+        m.crc = (q.vs[0] ^ q.vs[1]) ^ (q.vs[2] ^ q.vs[3]);
+        const uint32_t qp = (hi > 0u ? q.vs[0] : 0u) ^ (hi > 1u ? q.vs[1] : 0u) ^ (hi > 2u ? q.vs[2] : 0u);
+        if (has) a.span_bnd[first + src] = make_uint4(p1, cap, qp, item);
+      }
+      finish(valid, kRow, 0u, 1u, 0u, 0u, cidx, tsk, m);
     };
 
     if constexpr (kSB) {
@@ -1944,9 +2088,11 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         } while ((kS && steal) ? (c_more || p_ok) : p_ok);
       } else if constexpr (DEPTH == 1) {
         u32x4 bufA[4], bufB[4];
+        u32x4 recA = {0u, 0u, 0u, 0u}, recB = {0u, 0u, 0u, 0u}; // kSpan: the rows' block records
         issue(c_p0, c_lp, c_nr, c_r, c_ok, safe, bufA);
+        if constexpr (kSpan) recA = span_record(c_ok ? c_item : first_task);
         RPCCRC_ROWS_START();
-        auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4]) {
+        auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4], u32x4 &crec, u32x4 &nrec) {
           uint32_t m_item, m_lp;
           uint64_t m_p0;
           uint32_t m_r, m_len, m_z, m_nr, m_seed;
@@ -1954,7 +2100,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           succ(c_ok, c_more, c_item, c_r, c_nr, m_item, m_r, m_ok, m_more, m_p0, m_lp, m_len, m_z, m_nr, m_seed, c_p0,
                c_lp, c_len, c_z, c_seed);
           issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
-          compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
+          if constexpr (kSpan) {
+            nrec = span_record(m_ok ? m_item : first_task);
+            compute_span(c_ok, c_c, c_item, c_item, cb, crec);
+          } else {
+            compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
+          }
           publish();
           c_c = m_c;
           c_ok = m_ok;
@@ -1969,8 +2120,8 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
           c_nr = m_nr;
         };
         do {
-          step(bufA, bufB);
-          step(bufB, bufA);
+          step(bufA, bufB, recA, recB);
+          step(bufB, bufA, recB, recA);
         } while ((kS && steal) ? c_more : c_ok);
       } else {
         // DEPTH = 2: the next two rows' loads are in flight while one computes.
@@ -2018,7 +2169,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         } while (c_ok);
       }
     };
-    if constexpr (STEAL && !kTwoPhase) {
+    if constexpr (STEAL && (!kTwoPhase || kSpan)) { // (the span pass is device-counted: one loop)
       rows_phase(std::integral_constant<int, 3>{});
     } else if constexpr (STEAL) {
       // Device-counted launches (the big-body route's chunk and span passes)

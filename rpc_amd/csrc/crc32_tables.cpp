@@ -74,6 +74,23 @@ void build_big_dbl(uint32_t *tab) {
     }
 }
 
+void build_dense_tab(uint32_t *tab) {
+  auto put = [&](uint32_t map, uint32_t xp) { // [n][nib][map] of s -> s * xp mod P (crc32_layout.h)
+    for (uint32_t n = 0; n < 8; ++n)
+      for (uint32_t j = 0; j < 16; ++j) tab[(n * 16 + j) * kDenseMaps + map] = gf2_mulmod(xp, j << (4 * n));
+  };
+  for (uint32_t b = 0; b < 16; ++b) put(kDenseM4 + b, gf2_xpow(8ull * 4 * b));
+  for (uint32_t a = 0; a <= 16; ++a) put(kDenseM64 + a, gf2_xpow(8ull * 64 * a));
+  for (uint32_t h = 0; h < 4; ++h) put(kDenseMQ + h, gf2_xpow(8ull * 1024 * h));
+  for (uint32_t k = 0; k < 16; ++k) { // x^(-8 k unit) mod P: undo k units of zero bytes
+    put(kDenseMI0 + k, gf2_unshift_bytes(kX0, k));
+    put(kDenseMI1 + k, gf2_unshift_bytes(kX0, 16 * k));
+    put(kDenseMI2 + k, gf2_unshift_bytes(kX0, 256 * k));
+  }
+  for (uint32_t k = 0; k < 16; ++k) put(kDenseMB0 + k, gf2_xpow(8ull * 4096 * k));
+  for (uint32_t k = 0; k <= 16; ++k) put(kDenseMB1 + k, gf2_xpow(8ull * 65536 * k));
+}
+
 void build_scalar_tab(uint32_t *tab) {
   for (int k = 0; k < 4; ++k)
     for (uint32_t v = 0; v < 256; ++v) tab[256 * k + v] = crc_slice_entry(k, v);

@@ -336,6 +336,7 @@ struct DeviceCtx {
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
   uint32_t *big_dbl = nullptr; // the big-body fold's doubling maps per chunk class (build_big_dbl)
   uint4 *scalar_tab = nullptr; // one-wave scalar kernel's table image (kScalarTabWords)
+  uint32_t *dense_tab = nullptr; // the dense span fold's maps (kDenseTabWords, build_dense_tab)
   // Device error word (pinned, coherent host memory) of the ASYNCHRONOUS calls
   // (device batches, large bodies, frames): the rows kernel stores kErr* here
   // when a bounded wait runs out (crc32_rows.h).  Once it is non-zero, every
@@ -480,6 +481,7 @@ void init_device(int dev) {
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.big_dbl, kBigDblWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.scalar_tab, kScalarTabWords * 4) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.dense_tab, kDenseTabWords * 4) : e;
   e = (e == hipSuccess) ? hipHostMalloc(reinterpret_cast<void **>(&c.err), 64, hipHostMallocCoherent) : e;
   if (e == hipSuccess) *reinterpret_cast<volatile uint32_t *>(c.err) = 0;
   if (e == hipSuccess) {
@@ -505,6 +507,11 @@ void init_device(int dev) {
     e = hipMemcpy(c.big_dbl, dbl.data(), kBigDblWords * 4, hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipMemcpy(c.scalar_tab, stab.data(), kScalarTabWords * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    std::vector<uint32_t> dt(kDenseTabWords);
+    build_dense_tab(dt.data());
+    e = hipMemcpy(c.dense_tab, dt.data(), kDenseTabWords * 4, hipMemcpyHostToDevice);
+  }
   (void)hipSetDevice(prev);
   c.ws = new BlockPool(false, 1ull << 30);
   c.pin = new BlockPool(true, 256ull << 20);
@@ -637,6 +644,16 @@ bool ragged_steal() {
   return v;
 }
 
+// Dense span mode for bounded ragged batches.  RPCCRC_DENSE=0
+// turns it off (the rows pass only, as in rounds 1-5).
+bool dense_enabled() {
+  static const bool v = [] {
+    const char *e = getenv("RPCCRC_DENSE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // err: the error word of the call's launches (nullptr: the device's, for the
 // asynchronous entry points; the synchronous ones pass a word of their own).
 int items(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
@@ -672,7 +689,8 @@ struct FramesCmp {
 int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
            uint32_t mode, uint32_t *out, hipStream_t s, bool small_bodies, bool route, uint32_t *err = nullptr,
            uint64_t span_bytes = 0, const FramesCmp *cmp = nullptr, bool *compared = nullptr,
-           const FramesParse *fparse = nullptr, const FramesStamp *fstamp = nullptr, bool *stamped = nullptr) {
+           const FramesParse *fparse = nullptr, const FramesStamp *fstamp = nullptr, bool *stamped = nullptr,
+           uint32_t max_len = 0) {
   const int path = g_ragged_path.load(std::memory_order_relaxed);
   const bool nt = nontemporal();
   const int mb = max_blocks_for(c);
@@ -781,6 +799,30 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
       if (const int rc = ssl.get(c, span_rows, 1, s)) return rc;
     a.test_giveup = take_test_giveup(); // (the route's chunk pass; the plain rows pass takes its own below)
   }
+  // Dense span mode: a bounded batch (no big-body route) of
+  // many bodies whose bound allows it.  The plan decides on the device whether
+  // the bodies lie back to back in order with 64 B .. 1 MiB each; then the span
+  // pass and the fold compute every CRC and the rows pass below exits at once
+  // (DenseCtl::skip); otherwise the span pass and the fold exit at once.
+  const uint64_t nb_cap = std::min<uint64_t>(n * (uint64_t)max_len / 4096u + 2u, kDenseMaxBlocks);
+  const bool dense = dense_enabled() && !route && !split && !small_bodies && mode == kModeFinal && n >= kDenseMinN &&
+                     n <= kDenseMaxN && max_len >= kDenseMinBody && max_len <= kDenseMaxBody &&
+                     nb_cap >= 8ull * dyn_round(1) * (uint64_t)mb;
+  Lease dws;
+  DenseArgs dn{};
+  StealLease dsl; // the span pass's steal counter
+  if (dense) {
+    if (const int rc = dws.get(c.ws, dense_workspace_bytes(n, nb_cap), s)) return rc;
+    dn = dense_carve(dws.ptr(), n, nb_cap);
+    dn.base = base;
+    dn.offsets = offsets;
+    dn.lengths = lengths;
+    dn.out = out;
+    dn.tq = c.tq;
+    dn.tab = c.dense_tab;
+    RPCCRC_TRY(launch_dense_plan(dn, s));
+    a.skip_dev = &dn.ctl->skip;
+  }
   StealLease rsl; // the plain rows pass deals its tail from a steal counter too (RPCCRC_RAGGED_STEAL=0: not)
   if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
@@ -794,6 +836,19 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     RPCCRC_TRY(launch_rows(a, 1, nt, mb, s, rsl.done_event(), &rsl.recorded));
     a.steal = nullptr;
     a.test_giveup = route_giveup;
+  }
+  if (dense) {
+    ItemsArgs sp = items_args(c, nullptr, nullptr, nullptr, nb_cap, 4096, 4096, kModeRaw, dn.W);
+    if (err) sp.err = err;
+    sp.n_dev = &dn.ctl->nblocks;
+    sp.span_ctl = dn.ctl;
+    sp.span_rec = dn.rec;
+    sp.span_bpos = dn.bpos;
+    sp.span_bnd = dn.bnd;
+    if (const int rc = dsl.get(c, nb_cap, 1, s)) return rc;
+    sp.steal = dsl.p;
+    RPCCRC_TRY(launch_rows(sp, 1, nt, mb, s, dsl.done_event(), &dsl.recorded));
+    RPCCRC_TRY(launch_dense_fold(dn, c.cus, s));
   }
   if (route) {
     StealArgs span;
@@ -1514,7 +1569,8 @@ int rpc_crc32_device_batch_bounded(const uint8_t *d_base, const uint64_t *d_offs
   // are not launched.  A body over a wrong bound is still CRC'd correctly by
   // the rows pass (one wave for the whole body): the hint is about speed only.
   const bool route = max_len == 0 || max_len >= big_min_for(n);
-  return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream), false, route);
+  return ragged(*c, d_base, d_offsets, d_lengths, n, kModeFinal, d_out, static_cast<hipStream_t>(stream), false, route,
+                nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, max_len);
 }
 
 int rpc_crc32_device_uniform(const uint8_t *d_base, uint64_t n, uint32_t body_len, uint64_t stride, uint32_t *d_out,

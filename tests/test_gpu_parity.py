@@ -765,6 +765,97 @@ def test_c2_full_size_every_crc():
     assert rpc_amd.device_status() == 0
 
 
+def _dense_case(lens, pad=0, gap_at=None, seed=0xDE45, max_len=None):
+    """A batch of bodies back to back from byte `pad` of a buffer (a gap of 16 B
+    before body gap_at, if given), every CRC through the bounded call against the
+    oracle, and against the unbounded call (rows + route: no dense plan)."""
+    lens = np.asarray(lens, dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64) + np.uint64(pad)
+    if gap_at is not None:
+        offs[gap_at:] += np.uint64(16)
+    total = int(offs[-1]) + int(lens[-1])
+    # (at most 7 B of tail room, for fill_random's 8-B words: the span's last
+    # block is range-checked at the stream's 16-B end)
+    base = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
+    rpc_amd.fill_random(base, seed)
+    doffs, dlens = to_dev(offs.view(np.int64)), to_dev(lens.view(np.int32))
+    got = u32(rpc_amd.device_batch(base, doffs, dlens, max_len=int(lens.max()) if max_len is None else max_len))
+    torch.cuda.synchronize()
+    host = base.cpu().numpy()
+    want = oracle.crc32_batch_mt(host, offs, lens)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (bad[:10], lens[bad[:10]])
+    plain = u32(rpc_amd.device_batch(base, doffs, dlens))
+    assert np.array_equal(got, plain)
+    assert rpc_amd.device_status() == 0
+
+
+@pytest.mark.parametrize("case", ["loguniform", "tiny_dense", "block_ends", "pad7", "max_body", "mixed_runs"])
+def test_dense_span_mode(case):
+    """a bounded ragged batch whose bodies lie back to back in order,
+    each of 64 B - 1 MiB, takes the dense span pass (uniform 4 KiB blocks of the
+    whole stream + per-boundary values + a per-body fold).  Every CRC against the
+    oracle and against the rows path: log-uniform 64 B - 64 KiB (C2's shape), runs
+    of 64-100 B bodies (> 6 boundaries a block: the record's overflow path), bodies
+    ending exactly on block boundaries (and the stream's end on one), a stream
+    starting 7 B into its buffer (the anchor rounds down to 16 B), 1 MiB bodies (the
+    fold's longest Horner) and alternating runs of tiny and large bodies."""
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    n = 1 << 17
+    if case == "loguniform":
+        lens = oracle.loguniform_lengths(n, 0xD0E5)
+        _dense_case(lens)
+    elif case == "tiny_dense":
+        _dense_case(rng.integers(64, 101, n).astype(np.uint32))
+    elif case == "block_ends":
+        lens = np.full(n, 4096, dtype=np.uint32)
+        lens[0::3] = 4032
+        lens[1::3] = 64
+        lens[2::3] = 8192
+        _dense_case(lens)
+    elif case == "pad7":
+        _dense_case(rng.integers(64, 5000, n).astype(np.uint32), pad=7)
+    elif case == "max_body":
+        lens = rng.integers(64, 3000, n).astype(np.uint32)
+        lens[::997] = 1 << 20
+        _dense_case(lens)
+    else:
+        lens = np.where((np.arange(n) // 500) % 2 == 0, rng.integers(64, 128, n),
+                        rng.integers(20000, 65537, n)).astype(np.uint32)
+        _dense_case(lens)
+
+
+@pytest.mark.parametrize("case", ["gap", "short_body", "long_body", "unordered"])
+def test_dense_plan_falls_back(case):
+    """A bounded ragged batch the dense plan must refuse -- a 16-B gap between two
+    bodies, a 63-B body, a body over 1 MiB, bodies out of order -- is CRC'd by the
+    rows pass instead (decided on the device): every CRC against the oracle."""
+    rng = np.random.default_rng(7)
+    n = 1 << 17
+    lens = rng.integers(64, 3000, n).astype(np.uint32)
+    if case == "gap":
+        _dense_case(lens, gap_at=n // 2)
+    elif case == "short_body":
+        lens[n // 3] = 63
+        _dense_case(lens)
+    elif case == "long_body":  # (a bound below the truth: results never depend on it)
+        lens[n // 3] = (1 << 20) + 1
+        _dense_case(lens, max_len=65536)
+    else:
+        offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+        perm = np.arange(n)
+        perm[[10, 11]] = perm[[11, 10]]
+        offs, lens2 = offs[perm].copy(), lens[perm].copy()
+        total = int(lens.sum(dtype=np.uint64))
+        base = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
+        rpc_amd.fill_random(base, 0xABCD)
+        got = u32(rpc_amd.device_batch(base, to_dev(offs.view(np.int64)), to_dev(lens2.view(np.int32)),
+                                       max_len=int(lens.max())))
+        torch.cuda.synchronize()
+        want = oracle.crc32_batch_mt(base.cpu().numpy(), offs, lens2)
+        assert np.array_equal(got, want)
+
+
 def test_dyn_ragged_batch_with_huge_unrouted_body():
     """a DYN-sized ragged batch whose length bound (64 KiB)
     keeps a 512 MiB body off the big-body route, so ONE wave walks it (~0.1-0.3 s)
