@@ -67,7 +67,7 @@ struct ItemsArgs {
   const struct DenseCtl *span_ctl = nullptr;
   const uint4 *span_rec = nullptr;
   const uint16_t *span_bpos = nullptr;
-  uint4 *span_bnd = nullptr;
+  uint2 *span_bnd = nullptr;
   // Non-zero *skip_dev: the launch exits at once (the ragged rows pass of a
   // batch the dense plan took; decided on the device).
   const uint32_t *skip_dev = nullptr;
@@ -100,7 +100,9 @@ struct DenseCtl {
 // first kDenseInline boundaries.
 // Boundary g (body g's start; g = n: the last body's end) at stream offset
 // rel_g: bpos[g] = rel_g & 4095.  Span pass output per boundary:
-// bnd[g] = {P1, cap, Qp, block} (tests/test_dense_emu.py names them).
+// bnd[g] = {P1 ^ A_{64(15-lo)}(A_{4(16-tb)}(cap)), Qp} (tests/test_dense_emu.py
+// names them): crc0 of the boundary's quarter up to it, shifted to the quarter's
+// end, and the quarters before it shifted to the block's end.
 struct DenseArgs {
   const uint8_t *base;
   const uint64_t *offsets;
@@ -110,7 +112,7 @@ struct DenseArgs {
   DenseCtl *ctl;
   uint4 *rec;         // nb_cap
   uint16_t *bpos;     // n + 1
-  uint4 *bnd;         // n + 1
+  uint2 *bnd;         // n + 1
   uint32_t *W;        // nb_cap: crc0 of each block (the span pass's out)
   uint32_t *flags;    // dense_plan_blocks(n): the plan's per-workgroup "not dense" flags
   uint32_t *out;      // n CRCs

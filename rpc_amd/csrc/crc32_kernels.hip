@@ -1431,7 +1431,7 @@ hipError_t launch_stream_read(const void *p, uint64_t nbytes, int pattern, bool 
 // ---- dense span mode (tests/test_dense_emu.py restates it) ----
 
 size_t dense_workspace_bytes(uint64_t n, uint64_t nb_cap) {
-  return align256(sizeof(DenseCtl)) + align256(nb_cap * 16) + align256((n + 1) * 2) + align256((n + 1) * 16) +
+  return align256(sizeof(DenseCtl)) + align256(nb_cap * 16) + align256((n + 1) * 2) + align256((n + 1) * 8) +
          align256(nb_cap * 4) + align256(dense_plan_blocks(n) * 4);
 }
 
@@ -1448,7 +1448,7 @@ DenseArgs dense_carve(void *ws, uint64_t n, uint64_t nb_cap) {
   d.ctl = reinterpret_cast<DenseCtl *>(take(sizeof(DenseCtl)));
   d.rec = reinterpret_cast<uint4 *>(take(nb_cap * 16));
   d.bpos = reinterpret_cast<uint16_t *>(take((n + 1) * 2));
-  d.bnd = reinterpret_cast<uint4 *>(take((n + 1) * 16));
+  d.bnd = reinterpret_cast<uint2 *>(take((n + 1) * 8));
   d.W = reinterpret_cast<uint32_t *>(take(nb_cap * 4));
   d.flags = reinterpret_cast<uint32_t *>(take(dense_plan_blocks(n) * 4));
   return d;
@@ -1585,7 +1585,7 @@ __device__ __forceinline__ uint32_t dense_map(const uint32_t *t, uint32_t map, u
 }
 
 // Per boundary g: E = crc0(its block with the bytes from g on zeroed)
-//   = A_{1024(3-hi)}(P1 ^ A_{4(256 - 16 lo - tb)}(cap)) ^ Qp.
+//   = A_{1024(3-hi)}(bnd.x) ^ bnd.y  (the span pass stored the quarter part).
 // Per body g over blocks j .. j1 (D = j1 - j):
 //   j1 = j:  Y = Tq[4096 - off] ^ E(g) ^ E_end
 //   j1 > j:  Y = A_{4096 D}(Tq[4096 - off] ^ W[j] ^ E(g)) ^ X ^ E_end,
@@ -1606,13 +1606,27 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
   uint32_t *x_acc = s_x + wave * 64u;
   const uint64_t n = d.n, nw = (n + 62) / 63, last_w = d.nb_cap - 1;
   const uint64_t base = (uint64_t)(uintptr_t)d.base, anchor = d.ctl->anchor, rel_n = d.ctl->bytes;
-  for (uint64_t w = (uint64_t)blockIdx.x * 16u + wave; w < nw; w += (uint64_t)gridDim.x * 16u) {
+  // round trip 1 of a window: boundary g's offset and values, body g's length
+  // (every index clamped, no load under a branch); issued a window ahead, so
+  // it overlaps the current window's second round trip
+  const uint64_t wstep = (uint64_t)gridDim.x * 16u;
+  uint64_t w = (uint64_t)blockIdx.x * 16u + wave;
+  uint64_t nx_o = 0;
+  uint32_t nx_L = 0;
+  uint2 nx_b = make_uint2(0u, 0u);
+  auto fetch = [&](uint64_t ww) {
+    const uint64_t gg = 63u * min(ww, nw - 1) + lane;
+    nx_o = d.offsets[min(gg, n - 1)];
+    nx_L = d.lengths[min(gg, n - 1)];
+    nx_b = d.bnd[min(gg, n)];
+  };
+  if (w < nw) fetch(w);
+  for (; w < nw; w += wstep) {
     const uint64_t g = 63u * w + lane;
-    // round trip 1: boundary g's offset and values, body g's length (every
-    // index clamped, no load under a branch)
-    const uint64_t o = d.offsets[min(g, n - 1)];
-    const uint32_t L = d.lengths[min(g, n - 1)];
-    const uint4 b = d.bnd[min(g, n)];
+    const uint64_t o = nx_o;
+    const uint32_t L = nx_L;
+    const uint2 b = nx_b;
+    fetch(w + wstep); // (clamped: the last window again at the end)
     const bool body = lane < 63u && g < n;
     const uint64_t rs = g < n ? base + o - anchor : rel_n; // stream offset of boundary g
     const uint64_t j = rs >> 12;
@@ -1653,11 +1667,8 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
     const uint32_t wj1 = d.W[body ? min(j1, last_w) : 0u];
     const uint32_t wi0 = d.W[min(i0, last_w)];
     x_acc[lane] = 0u;
-    const uint32_t k = off >> 6, hi = k >> 4, lo = k & 15u, tb = (off & 63u) >> 2;
-    const uint32_t n1 = 256u - 16u * lo - tb; // 1 .. 256
-    uint32_t y = dense_map(s_tab, kDenseM4 + (n1 & 15u), b.y);
-    y = dense_map(s_tab, kDenseM64 + (n1 >> 4), y);
-    const uint32_t E = dense_map(s_tab, kDenseMQ + (3u - hi), b.x ^ y) ^ b.z;
+    const uint32_t hi = off >> 10;
+    const uint32_t E = dense_map(s_tab, kDenseMQ + (3u - hi), b.x) ^ b.y;
     const uint32_t En = (uint32_t)__shfl_down((int)E, 1, 64);
     if (lane < K) {
       uint32_t c = dense_map(s_tab, kDenseMB0 + (dist0 & 15u), wi0);

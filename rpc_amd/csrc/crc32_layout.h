@@ -62,6 +62,15 @@ constexpr uint32_t kLdsRoundMaps = kLdsZI2 + 11 * 512;
 static_assert(kLdsRoundMaps % 256 == 0 && kLdsRoundMaps + 4 * 512 <= kLdsTQ16, "round maps inside ZI");
 // A zero dword (TQ16's 12-byte tail pad): lanes with nothing to look up read it.
 constexpr uint32_t kLdsZero = kLdsTQ16 + 1028;
+// The dense span pass's image (crc32_rows.h kRowsSpanBnd; RAW 4096-byte rows
+// never read ZI or TQ16): over ZI..TQ16, the maps A_{4(16-tb)}, tb = 0..15 --
+// a boundary's chain state cap shifted to its 64-B segment's end -- word
+// (n * 16 + nib) * 17 + tb (stride 17: the lanes of one lookup, each with its
+// own tb, spread over the banks), below kLdsZero.
+constexpr uint32_t kLdsSpanM4 = kLdsZI2;
+constexpr uint32_t kSpanM4Stride = 17;
+static_assert(kLdsSpanM4 + 128 * kSpanM4Stride * 4 <= kLdsZero, "span maps below the zero dword");
+void build_lds_image_span(uint32_t *img /* a V2 image: the maps go over its ZI / TQ16 */);
 static_assert(kLdsTQ16 + 1040 == kLdsBytesV2, "rows image size");
 static_assert(kLdsBytesV2 % 16 == 0 && kLdsBytesV2 <= 163840, "fits the 160 KiB LDS");
 // ---- sub-row shifts (ragged QB = 1 kernels only: image V3 = V2 + pad + SQ) ----
@@ -111,11 +120,11 @@ void build_big_dbl(uint32_t *tab /* kBigDblWords */);
 // The dense span fold's maps (crc32_kernels.hip dense_fold_kernel, DESIGN.md
 // 4.9), stored [n][nib][map] (word (n * 16 + nib) * kDenseMaps + map: the
 // lanes of one lookup, each with its own map, spread over all 32 banks; a
-// [map][n][nib] layout put one lookup on 16 banks): A_{4b} (b = 0..15), A_{64a} (a = 0..16),
-// A_{1024h} (h = 0..3), A_{-z0}, A_{-16 z1}, A_{-256 z2} (0..15 each),
-// A_{4096 d0} (d0 = 0..15), A_{65536 d1} (d1 = 0..16).
-constexpr uint32_t kDenseM4 = 0, kDenseM64 = 16, kDenseMQ = 33, kDenseMI0 = 37, kDenseMI1 = 53, kDenseMI2 = 69,
-                   kDenseMB0 = 85, kDenseMB1 = 101, kDenseMaps = 118;
+// [map][n][nib] layout put one lookup on 16 banks): A_{1024h} (h = 0..3),
+// A_{-z0}, A_{-16 z1}, A_{-256 z2} (0..15 each), A_{4096 d0} (d0 = 0..15),
+// A_{65536 d1} (d1 = 0..16).
+constexpr uint32_t kDenseMQ = 0, kDenseMI0 = 4, kDenseMI1 = 20, kDenseMI2 = 36, kDenseMB0 = 52, kDenseMB1 = 68,
+                   kDenseMaps = 85;
 constexpr uint32_t kDenseTabWords = kDenseMaps * 128;
 void build_dense_tab(uint32_t *tab /* kDenseTabWords */);
 

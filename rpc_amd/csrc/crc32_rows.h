@@ -420,6 +420,16 @@ constexpr int kRowsRoundOut = 32768;
 // in-quarter prefix P1, the chain state cap at the boundary's dword and the
 // quarter prefix Qp (tests/test_dense_emu.py), from values the lanes hold.
 constexpr int kRowsSpanBnd = 131072;
+// A/B builds of the span pass: RPCCRC_SPAN_TWO_PHASE=1 runs it as two phases
+// (the plain loop, then the pool loop) like host-counted stealing launches;
+// RPCCRC_SPAN_ABL=1 never takes the boundary path, 2 also skips the record
+// load (timing only: wrong CRCs).
+#ifndef RPCCRC_SPAN_TWO_PHASE
+#define RPCCRC_SPAN_TWO_PHASE 0
+#endif
+#ifndef RPCCRC_SPAN_ABL
+#define RPCCRC_SPAN_ABL 0
+#endif
 // QB = 1 software pipeline over rows (chain of row r+1 beside the merge of row r).
 #ifndef RPCCRC_ROWS_PIPE
 #define RPCCRC_ROWS_PIPE 1
@@ -642,6 +652,15 @@ __device__ __forceinline__ uint32_t seg_crc_cap(const uint8_t *lds, const u32x4 
     }
   cap = c;
   return slice4(lds, x, lsel);
+}
+// A_{4(16-tb)}(s): a boundary's captured chain state shifted to its segment's
+// end (the span image's maps at kLdsSpanM4, word (n * 16 + nib) * 17 + tb).
+__device__ __forceinline__ uint32_t span_m4(const uint8_t *lds, uint32_t s, uint32_t tb) {
+  uint32_t t[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k)
+    t[k] = lds_ld(lds, kLdsSpanM4 + 4u * ((k * 16u + ((s >> (4u * k)) & 15u)) * kSpanM4Stride + tb));
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
 }
 // Inclusive XOR scan over the 16 lanes of each DPP row (row_shr, zeros shifted in).
 __device__ __forceinline__ uint32_t row_xor_scan(uint32_t v) {
@@ -1399,7 +1418,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     auto compute_span = [&](bool valid, uint32_t cidx, uint32_t tsk, uint32_t item, u32x4 (&buf)[4],
                             const u32x4 &recv) {
       const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)recv[0]);
-      const uint32_t first = r0 & 0x1FFFFFFu, cnt = r0 >> 25;
+      const uint32_t first = r0 & 0x1FFFFFFu, cnt = RPCCRC_SPAN_ABL ? 0u : r0 >> 25;
       transpose(buf);
       RowMerge m;
       m.rwu = 0u;
@@ -1452,7 +1471,10 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         const RowQuarterVals q = merge_quarters(lds, v, dl);
         m.crc = (q.vs[0] ^ q.vs[1]) ^ (q.vs[2] ^ q.vs[3]);
         const uint32_t qp = (hi > 0u ? q.vs[0] : 0u) ^ (hi > 1u ? q.vs[1] : 0u) ^ (hi > 2u ? q.vs[2] : 0u);
-        if (has) a.span_bnd[first + src] = make_uint4(p1, cap, qp, item);
+        // the boundary's quarter up to it, shifted to the quarter's end:
+        // P1 ^ A_{64(15-lo)}(A_{4(16-tb)}(cap)) (cap = 0 in the other lanes)
+        const uint32_t eq = p1 ^ st1_map(lds, span_m4(lds, cap, has ? rr >> 2 : 0u), lsel1);
+        if (has) a.span_bnd[first + src] = make_uint2(eq, qp);
       }
       finish(valid, kRow, 0u, 1u, 0u, 0u, cidx, tsk, m);
     };
@@ -2090,7 +2112,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         u32x4 bufA[4], bufB[4];
         u32x4 recA = {0u, 0u, 0u, 0u}, recB = {0u, 0u, 0u, 0u}; // kSpan: the rows' block records
         issue(c_p0, c_lp, c_nr, c_r, c_ok, safe, bufA);
-        if constexpr (kSpan) recA = span_record(c_ok ? c_item : first_task);
+        if constexpr (kSpan && RPCCRC_SPAN_ABL < 2) recA = span_record(c_ok ? c_item : first_task);
         RPCCRC_ROWS_START();
         auto step = [&](u32x4 (&cb)[4], u32x4 (&nb)[4], u32x4 &crec, u32x4 &nrec) {
           uint32_t m_item, m_lp;
@@ -2101,7 +2123,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
                c_lp, c_len, c_z, c_seed);
           issue(m_p0, m_lp, m_nr, m_r, m_ok, safe, nb);
           if constexpr (kSpan) {
-            nrec = span_record(m_ok ? m_item : first_task);
+            if constexpr (RPCCRC_SPAN_ABL < 2) nrec = span_record(m_ok ? m_item : first_task);
             compute_span(c_ok, c_c, c_item, c_item, cb, crec);
           } else {
             compute(c_ok, c_lp, c_len, c_z, c_nr, c_r, c_seed, c_c, c_item, cb);
@@ -2169,7 +2191,7 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
         } while (c_ok);
       }
     };
-    if constexpr (STEAL && (!kTwoPhase || kSpan)) { // (the span pass is device-counted: one loop)
+    if constexpr (STEAL && (!kTwoPhase || (kSpan && !RPCCRC_SPAN_TWO_PHASE))) { // (the span pass is device-counted: one loop)
       rows_phase(std::integral_constant<int, 3>{});
     } else if constexpr (STEAL) {
       // Device-counted launches (the big-body route's chunk and span passes)

@@ -79,8 +79,6 @@ void build_dense_tab(uint32_t *tab) {
     for (uint32_t n = 0; n < 8; ++n)
       for (uint32_t j = 0; j < 16; ++j) tab[(n * 16 + j) * kDenseMaps + map] = gf2_mulmod(xp, j << (4 * n));
   };
-  for (uint32_t b = 0; b < 16; ++b) put(kDenseM4 + b, gf2_xpow(8ull * 4 * b));
-  for (uint32_t a = 0; a <= 16; ++a) put(kDenseM64 + a, gf2_xpow(8ull * 64 * a));
   for (uint32_t h = 0; h < 4; ++h) put(kDenseMQ + h, gf2_xpow(8ull * 1024 * h));
   for (uint32_t k = 0; k < 16; ++k) { // x^(-8 k unit) mod P: undo k units of zero bytes
     put(kDenseMI0 + k, gf2_unshift_bytes(kX0, k));
@@ -89,6 +87,18 @@ void build_dense_tab(uint32_t *tab) {
   }
   for (uint32_t k = 0; k < 16; ++k) put(kDenseMB0 + k, gf2_xpow(8ull * 4096 * k));
   for (uint32_t k = 0; k <= 16; ++k) put(kDenseMB1 + k, gf2_xpow(8ull * 65536 * k));
+}
+
+void build_lds_image_span(uint32_t *img) {
+  uint8_t *b = reinterpret_cast<uint8_t *>(img);
+  for (uint32_t tb = 0; tb < 16; ++tb) {
+    const uint32_t xp = gf2_xpow(8ull * 4 * (16 - tb));
+    for (uint32_t n = 0; n < 8; ++n)
+      for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t v = gf2_mulmod(xp, j << (4 * n));
+        memcpy(b + kLdsSpanM4 + 4 * ((n * 16 + j) * kSpanM4Stride + tb), &v, 4);
+      }
+  }
 }
 
 void build_scalar_tab(uint32_t *tab) {

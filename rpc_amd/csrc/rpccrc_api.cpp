@@ -332,6 +332,7 @@ struct DeviceCtx {
   int cus = 0;
   uint4 *img = nullptr; // LDS table image (rows kernel layout, 155 KiB)
   uint4 *img_round = nullptr; // the same with the round maps in ZI[11..14] (crc32_layout.h kLdsRoundMaps)
+  uint4 *img_span = nullptr;  // the same with the dense span pass's maps over ZI / TQ16 (kLdsSpanM4)
   uint32_t *tq = nullptr;
   uint4 *shift_nib = nullptr; // NIB[k][i][j] = A_{2^k bytes}(j << 4i) (chunk combine)
   uint32_t *big_dbl = nullptr; // the big-body fold's doubling maps per chunk class (build_big_dbl)
@@ -477,6 +478,7 @@ void init_device(int dev) {
   hipError_t e = hipSuccess;
   e = (e == hipSuccess) ? hipMalloc(&c.img, kImgHbmBytes) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.img_round, kImgHbmBytes) : e;
+  e = (e == hipSuccess) ? hipMalloc(&c.img_span, kImgHbmBytes) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.tq, kTqEntries * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.shift_nib, kShiftNibWords * 4) : e;
   e = (e == hipSuccess) ? hipMalloc(&c.big_dbl, kBigDblWords * 4) : e;
@@ -498,6 +500,9 @@ void init_device(int dev) {
     };
     e = upload(c.img, img);
     if (e == hipSuccess) e = upload(c.img_round, img_round);
+    std::vector<uint32_t> img_span(img);
+    build_lds_image_span(img_span.data());
+    if (e == hipSuccess) e = upload(c.img_span, img_span);
   }
   if (e == hipSuccess) e = hipMemcpy(c.tq, tq.data(), kTqEntries * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c.shift_nib, nib.data(), kShiftNibWords * 4, hipMemcpyHostToDevice);
@@ -841,6 +846,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     ItemsArgs sp = items_args(c, nullptr, nullptr, nullptr, nb_cap, 4096, 4096, kModeRaw, dn.W);
     if (err) sp.err = err;
     sp.n_dev = &dn.ctl->nblocks;
+    sp.lds_image = c.img_span;
     sp.span_ctl = dn.ctl;
     sp.span_rec = dn.rec;
     sp.span_bpos = dn.bpos;

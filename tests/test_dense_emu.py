@@ -11,8 +11,9 @@ anyway:
     cap = X_tb ^ (w_tb & ~low_u)                (the segment's chain state at
           b's dword, its bytes at or after b removed)
     Qp  = XOR over the quarters before b's of A_{1024(3-h)}(v_h)
-The fold then forms, per boundary, E(b) = crc0(block with bytes >= b zeroed)
-    E = A_{1024(3-hi)}(P1 ^ A_{4(256 - 16 lo - tb)}(cap)) ^ Qp
+The span pass stores eq = P1 ^ A_{64(15-lo)}(A_{4(16-tb)}(cap)) and Qp; the fold
+then forms, per boundary, E(b) = crc0(block with bytes >= b zeroed)
+    E = A_{1024(3-hi)}(eq) ^ Qp
 and per body [s, e) over blocks j0 .. j1 (D = j1 - j0 > 0):
     Y = A_{4096 D}(Tq[4096 - s_off] ^ W[j0] ^ E(s)) ^ X ^ E(e)
     X = XOR over the blocks j in between of A_{4096 (j1 - j)}(W[j])
@@ -135,12 +136,13 @@ def span_block(block: bytes, offs):
 
 
 def boundary_e(off, p1, cap, qp):
-    """dense_fold_kernel: E(b) = crc0(block with bytes >= b zeroed)."""
+    """E(b) = crc0(block with bytes >= b zeroed): the span pass stores
+    eq = P1 ^ A_{64(15-lo)}(A_{4(16-tb)}(cap)) (its span_m4 and st1_map lookups)
+    and Qp; dense_fold_kernel adds the quarter shift A_{1024(3-hi)}."""
     k, rr = off >> 6, off & 63
     hi, lo, tb = k >> 4, k & 15, rr >> 2
-    n1 = 256 - 16 * lo - tb  # 1..256
-    y = A(64 * (n1 >> 4), A(4 * (n1 & 15), cap))  # the fold's two maps
-    return A(1024 * (3 - hi), p1 ^ y) ^ qp
+    eq = p1 ^ A(64 * (15 - lo), A(4 * (16 - tb), cap))
+    return A(1024 * (3 - hi), eq) ^ qp
 
 
 def dense_emulated(stream: bytes, anchor_pad: int, lens):
