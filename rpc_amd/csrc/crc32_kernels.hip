@@ -1461,6 +1461,37 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
   return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ uint64_t ballot64(bool p) { return (uint64_t)__builtin_amdgcn_ballot_w64(p); }
+// Lane-to-lane words through LDS inside one wave: atomic (relaxed, wavefront
+// scope) stores and loads with a wave barrier between the phases.  Plain ones
+// are a data race to the compiler: it forwarded a lane's own earlier store to
+// its load where the other lanes' stores were to reach it (owner marks read as
+// 0: wrong dense CRCs, found by tests/test_gpu_parity.py test_dense_span_mode).
+__device__ __forceinline__ void lane_st(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+__device__ __forceinline__ uint32_t lane_ld(uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// Inclusive wave scans on the VALU: row_shr 1, 2, 4, 8 (DPP) inside each
+// 16-lane row, then the row totals (lanes 15, 31, 47) read as scalars and
+// added to the rows after them (gfx950 has no DPP row_bcast 15 / 31: the
+// first version of this scan used them and came out wrong).  A ds_bpermute
+// per step cost LDS issue slots the fold's lookups need.
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  auto op = [](uint32_t a, uint32_t b) { return MAX ? max(a, b) : a + b; };
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true)); // row_shr:1 (zeros shifted in)
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xF, 0xF, true)); // row_shr:2 (zeros shifted in)
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xF, 0xF, true)); // row_shr:4 (zeros shifted in)
+  v = op(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x118, 0xF, 0xF, true)); // row_shr:8 (zeros shifted in)
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+  const uint32_t r1 = op(r0, (uint32_t)__builtin_amdgcn_readlane((int)v, 31));
+  const uint32_t r2 = op(r1, (uint32_t)__builtin_amdgcn_readlane((int)v, 47));
+  const uint32_t row = (threadIdx.x & 63u) >> 4;
+  const uint32_t add = row == 0u ? 0u : (row == 1u ? r0 : (row == 2u ? r1 : r2));
+  return row == 0u ? v : op(v, add);
+}
 
 // Decides whether the batch is dense -- every body kDenseMinBody ..
 // kDenseMaxBody bytes and starting where the previous one ends -- and writes
@@ -1476,6 +1507,7 @@ __device__ __forceinline__ uint64_t ballot64(bool p) { return (uint64_t)__builti
 // lanes.  Each workgroup stores whether it found the batch not dense
 // (dense_decide_kernel reads them).
 __global__ __launch_bounds__(256) void dense_plan_kernel(DenseArgs d) {
+  __shared__ uint32_t s_own[4 * 64];
   const uint64_t n = d.n;
   const uint64_t base = (uint64_t)(uintptr_t)d.base;
   const uint64_t anchor = (base + d.offsets[0]) & ~(uint64_t)15;
@@ -1528,22 +1560,29 @@ __global__ __launch_bounds__(256) void dense_plan_kernel(DenseArgs d) {
     uint32_t k = 0;
     if (va && first && g != 0 && ja > jp + 1u && ja - jp <= (kDenseMaxBody >> 12) + 2)
       k = (uint32_t)(min(ja, nblocks) > jp + 1u ? min(ja, nblocks) - jp - 1u : 0u);
-    uint32_t incl = k;
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)incl, dd, 64);
-      if ((int)lane >= dd) incl += t;
-    }
-    const uint32_t K = (uint32_t)__shfl((int)incl, 63, 64);
+    const uint32_t incl = wave_incl_scan<false>(k);
+    const uint32_t K = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // the first pass's owners by marks and a max-scan (fold kernel), later
+    // passes by a search
+    uint32_t *own_mark = s_own + (threadIdx.x >> 6) * 64u;
+    lane_st(&own_mark[lane], 0u);
+    __builtin_amdgcn_wave_barrier();
+    if (k != 0u && incl - k < 64u) lane_st(&own_mark[incl - k], lane);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t own0 = wave_incl_scan<true>(lane_ld(&own_mark[lane]));
+    __builtin_amdgcn_wave_barrier();
     for (uint32_t q0 = 0; q0 < K; q0 += 64u) {
       const uint32_t q = q0 + lane;
-      uint32_t own = 0; // the first lane whose inclusive sum passes q
+      uint32_t own = own0;
+      if (q0 != 0u) { // (the first lane whose inclusive sum passes q)
+        own = 0;
 #pragma unroll
-      for (uint32_t step = 32; step; step >>= 1) {
-        const uint32_t v = (uint32_t)__shfl((int)incl, (int)(own + step - 1u), 64);
-        if (v <= q) own += step;
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t v = (uint32_t)__shfl((int)incl, (int)(own + step - 1u), 64);
+          if (v <= q) own += step;
+        }
+        own = min(own, 63u);
       }
-      own = min(own, 63u);
       const uint64_t jp_o = shfl64(jp, (int)own);
       const uint32_t ex_o = (uint32_t)__shfl((int)(incl - k), (int)own, 64);
       const uint64_t j = jp_o + 1u + (q - ex_o);
@@ -1599,6 +1638,7 @@ __device__ __forceinline__ uint32_t dense_map(const uint32_t *t, uint32_t map, u
 __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
   __shared__ uint32_t s_tab[kDenseTabWords];
   __shared__ uint32_t s_x[16 * 64];
+  __shared__ uint32_t s_own[16 * 64];
   if (d.ctl->nblocks == 0u) return; // (block-uniform) not dense: the rows pass did it
   for (uint32_t i = threadIdx.x; i < kDenseTabWords; i += 1024u) s_tab[i] = d.tab[i];
   __syncthreads();
@@ -1636,15 +1676,17 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
     const uint32_t e_off = (uint32_t)(re - j1 * 4096u); // 1 .. 4096
     // the blocks in between: m per body, dealt over the wave's lanes
     const uint32_t m = (body && j1 > j + 1u) ? (uint32_t)(j1 - j - 1u) : 0u;
-    uint32_t incl = m;
-#pragma unroll
-    for (int dd = 1; dd < 64; dd <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)incl, dd, 64);
-      if ((int)lane >= dd) incl += t;
-    }
-    const uint32_t K = (uint32_t)__shfl((int)incl, 63, 64);
+    const uint32_t incl = wave_incl_scan<false>(m);
+    const uint32_t K = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     // lane q's in-between block for pass q0: its body (owner), index and distance
-    auto deal = [&](uint32_t q0, uint64_t &i, uint32_t &dist, uint32_t &own) {
+    auto deal_from = [&](uint32_t q, uint32_t own, uint64_t &i, uint32_t &dist) {
+      const uint32_t jo = (uint32_t)__shfl((int)(uint32_t)j, (int)own, 64); // (blocks < 2^24)
+      const uint32_t j1o = (uint32_t)__shfl((int)(uint32_t)j1, (int)own, 64);
+      const uint32_t exo = (uint32_t)__shfl((int)(incl - m), (int)own, 64);
+      i = q < K ? (uint64_t)jo + 1u + (q - exo) : 0u;
+      dist = q < K ? j1o - (uint32_t)i : 0u; // 1 .. 256
+    };
+    auto deal = [&](uint32_t q0, uint64_t &i, uint32_t &dist, uint32_t &own) { // (passes past the first)
       const uint32_t q = q0 + lane;
       own = 0; // the first lane whose inclusive sum passes q
 #pragma unroll
@@ -1653,20 +1695,26 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
         if (v <= q) own += step;
       }
       own = min(own, 63u);
-      const uint64_t jo = shfl64(j, (int)own), j1o = shfl64(j1, (int)own);
-      const uint32_t exo = (uint32_t)__shfl((int)(incl - m), (int)own, 64);
-      i = q < K ? jo + 1u + (q - exo) : 0u;
-      dist = q < K ? (uint32_t)(j1o - i) : 0u; // 1 .. 256
+      deal_from(q, own, i, dist);
     };
+    // the first pass: each owner marks the slot of its first block, a max-scan
+    // spreads the marks (an LDS store and load instead of a 6-step search)
+    uint32_t *own_mark = s_own + wave * 64u;
+    lane_st(&own_mark[lane], 0u);
+    __builtin_amdgcn_wave_barrier();
+    if (m != 0u && incl - m < 64u) lane_st(&own_mark[incl - m], lane);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t own0 = wave_incl_scan<true>(lane_ld(&own_mark[lane]));
     uint64_t i0;
-    uint32_t dist0, own0;
-    deal(0u, i0, dist0, own0);
+    uint32_t dist0;
+    deal_from(lane, own0, i0, dist0);
     // round trip 2: seed, first / last block CRCs, the first pass's blocks
     const uint32_t tqv = d.tq[4096u - off];
     const uint32_t wj = d.W[body ? min(j, last_w) : 0u];
     const uint32_t wj1 = d.W[body ? min(j1, last_w) : 0u];
     const uint32_t wi0 = d.W[min(i0, last_w)];
-    x_acc[lane] = 0u;
+    lane_st(&x_acc[lane], 0u);
+    __builtin_amdgcn_wave_barrier();
     const uint32_t hi = off >> 10;
     const uint32_t E = dense_map(s_tab, kDenseMQ + (3u - hi), b.x) ^ b.y;
     const uint32_t En = (uint32_t)__shfl_down((int)E, 1, 64);
@@ -1686,7 +1734,8 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
         __hip_atomic_fetch_xor(&x_acc[own], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       }
     }
-    const uint32_t X = x_acc[lane];
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t X = lane_ld(&x_acc[lane]);
     if (body) {
       const uint32_t Ee = e_off == 4096u ? wj1 : En;
       uint32_t acc = tqv ^ E;
