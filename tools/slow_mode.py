@@ -34,12 +34,21 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--prewarm-s", type=float, default=0.5)
     ap.add_argument("--blocks", type=int, default=1, help="consecutive timed blocks per round (a ramp shows as a trend)")
+    ap.add_argument("--stride-kib", type=int, default=0,
+                    help="uniform configs: bodies this far apart (the same bytes over a wider address range)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream()
     for r in range(a.rounds):
         t_alloc = time.perf_counter()
         w = Workload(a.config, 0, dev)
+        if a.stride_kib and w.kind == "uniform":  # the same bodies, spread: base i * stride
+            import rpc_amd
+            stride = a.stride_kib * 1024
+            big = torch.empty(w.n * stride, dtype=torch.uint8, device=dev)
+            rpc_amd.fill_random(big, 0x51DE)
+            w.base = big
+            w.step = lambda w=w, stride=stride: rpc_amd.device_uniform(w.base, w.n, w.L, stride=stride, out=w.out)
         torch.cuda.synchronize()
         t_alloc = time.perf_counter() - t_alloc
         t0 = time.perf_counter()
@@ -57,7 +66,7 @@ def main():
         ev[-1].synchronize()
         us = [ev[b].elapsed_time(ev[b + 1]) * 1e3 / a.steps for b in range(a.blocks)]
         ptr = w.base.data_ptr() if hasattr(w, "base") else 0
-        print(json.dumps({"tag": a.tag, "pid": os.getpid(), "config": a.config, "round": r,
+        print(json.dumps({"tag": a.tag, "pid": os.getpid(), "config": a.config, "stride_kib": a.stride_kib, "round": r,
                           "us_per_launch": [round(x, 1) for x in us],
                           "frac": [round(w.algo_bytes / (x * 1e-6) / 8e12, 4) for x in us], "prewarm_launches": n_pw,
                           "since_start_s": round(time.perf_counter() - T0, 2),
