@@ -3,9 +3,10 @@
 
 Metric (BASELINE.json): "GiB/s CRC32 over device-resident batched bodies;
 1/2/4/8 MI355X".  A step = one pass of the batched CRC over the rank's batch
-(one launch of the HIP items kernel).  Default workload = the north star:
-1M x 4 KiB bodies per GPU (weak scaling), synthetic splitmix64 bytes generated
-on the device.  Other BASELINE configs: --config c1 | c2 | c3 | c4.
+(one launch of the HIP rows kernel; C2: the dense span step's launches,
+DESIGN.md 4.9).  Default workload = the north star: 1M x 4 KiB bodies per GPU
+(weak scaling), synthetic splitmix64 bytes generated on the device.  Other
+BASELINE configs: --config c1 | c2 | c3 | c4.
 
 Launch: python bench.py [--gpus N --steps K --warmup W].  N>1: one process per
 GPU under torch.distributed.run -- either the driver's own launch, or, when
@@ -592,6 +593,12 @@ def pick_launch_traffic(fetch, write):
     return f, statistics.median([x for x in w if x >= 0.5 * w[len(w) // 2]])
 
 
+# Kernels of a product step besides the rows kernel (the dense
+# span step; 4.3: the large-body combine).  The ragged rows pass that exits at
+# once in dense mode is a rows-kernel dispatch: pick_launch_traffic drops it.
+AUX_KERNELS = ("dense_plan_kernel", "dense_decide_kernel", "dense_fold_kernel", "crc32_chunk_combine")
+
+
 def live_traffic(args, algo_bytes: int):
     """HBM bytes per launch of the dominant kernel, measured in this run: two
     rocprofv3 PMC passes (FETCH_SIZE, then WRITE_SIZE -- separate runs, as
@@ -610,9 +617,12 @@ def live_traffic(args, algo_bytes: int):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None, "rocprofv3 not found"
+    import statistics
+
     tmp = tempfile.mkdtemp(prefix="rpccrc_pmc_")
     vals = {}
     seq = {}
+    aux_med = {}
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, counter)
@@ -627,20 +637,35 @@ def live_traffic(args, algo_bytes: int):
             if p.returncode != 0:
                 return None, f"rocprofv3 --pmc {counter} rc={p.returncode}: {(p.stderr or '')[-200:]}"
             per = {}
+            aux = {k: {} for k in AUX_KERNELS}
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
-                    if r["Counter_Name"] == counter and "crc32_rows_kernel" in r["Kernel_Name"]:
-                        per[(f, r["Dispatch_Id"])] = per.get((f, r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+                    if r["Counter_Name"] != counter:
+                        continue
+                    key = (f, r["Dispatch_Id"])
+                    if "crc32_rows_kernel" in r["Kernel_Name"]:
+                        per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+                    for a in AUX_KERNELS:
+                        if a in r["Kernel_Name"]:
+                            aux[a][key] = aux[a].get(key, 0.0) + float(r["Counter_Value"])
             if not per:
                 return None, f"no {counter} rows for crc32_rows_kernel"
             seq[counter] = [per[k] for k in sorted(per, key=lambda k: (k[0], int(k[1])))]
+            aux_med[counter] = {a: statistics.median(v.values()) for a, v in aux.items() if v}
         vals["FETCH_SIZE"], vals["WRITE_SIZE"] = pick_launch_traffic(seq["FETCH_SIZE"], seq["WRITE_SIZE"])
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    hbm = 2.0 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024
+    rows = 2.0 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024
+    # the step's other kernels (dense plan / decide / fold, the large-body
+    # combine): the median per dispatch of each, added to the rows launch
+    steps_aux = {a: 2.0 * aux_med["FETCH_SIZE"].get(a, 0.0) * 1024 + aux_med["WRITE_SIZE"].get(a, 0.0) * 1024
+                 for a in sorted(set(aux_med["FETCH_SIZE"]) | set(aux_med["WRITE_SIZE"]))}
+    hbm = rows + sum(steps_aux.values())
     return {"hbm_bytes_per_launch": hbm, "over_algorithmic": round(hbm / algo_bytes, 4),
-            "fetch_size_kib": vals["FETCH_SIZE"], "write_size_kib": vals["WRITE_SIZE"]}, \
-        "live: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this config (2 x FETCH_SIZE + WRITE_SIZE, KiB)"
+            "fetch_size_kib": vals["FETCH_SIZE"], "write_size_kib": vals["WRITE_SIZE"],
+            "rows_kernel_bytes": rows, "other_kernels_bytes": {a: round(b) for a, b in steps_aux.items()}}, \
+        ("live: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes of this config (2 x FETCH_SIZE + WRITE_SIZE, KiB), "
+         "the rows launch plus the median dispatch of each other kernel of the step")
 
 
 def rank_timing(dist, device, wall: float, kernel_s: float, median_s: float, total: int):
@@ -913,7 +938,10 @@ def main():
                 "traffic_detail": traffic_rec,
                 "kernel": {"uniform": "crc32_rows_kernel",
                            "ragged": "crc32_packed_kernel (+count/scan/plan)" if args.ragged_path == "packed"
-                           else "crc32_rows_kernel",
+                           else ("the dense span step: dense_plan + dense_decide + crc32_rows_kernel (rows pass, "
+                                 "exits at once) + crc32_rows_kernel (span pass) + dense_fold, timed as one step"
+                                 if os.environ.get("RPCCRC_DENSE", "1") != "0" and args.ragged_path in ("auto", "rows")
+                                 else "crc32_rows_kernel"),
                            "large": "crc32_rows_kernel (+chunk combine)"}[w.kind],
                 "median_source": median_src,
                 # the achieved rate against a streaming read of the

@@ -890,8 +890,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
   if (blockIdx.x == 0 && threadIdx.x < a.zero_n) a.zero_out[threadIdx.x] = 0u;
   if (a.n_dev != nullptr && ld_const(a.n_dev, 0) == 0) return;
   if (a.skip_dev != nullptr && ld_const(a.skip_dev, 0) != 0u) return; // (a dense batch: the span pass has it)
-  uint64_t t_entry = 0, t_image = 0;
-  if constexpr ((ABL & kRowsAblTimes) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_entry = 0, t_image = 0, c_entry = 0;
+  if constexpr ((ABL & kRowsAblTimes) != 0) { // (+ the shader clock: s_memtime ticks shader cycles)
+    t_entry = __builtin_amdgcn_s_memrealtime();
+    c_entry = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
+  }
   // All of this thread's image loads in flight at once (a rolled loop would
   // pay one L2 round trip per 16 KiB before the first HBM byte is read).
   // kEarly: the image in registers until the first row's loads are issued
@@ -2215,11 +2219,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       // (ragged batches need their offsets: the probe passes the times array in round_out)
       uint64_t *times = RAGGED ? reinterpret_cast<uint64_t *>(a.round_out) : const_cast<uint64_t *>(a.offsets);
       const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
+      const uint64_t c_exit = __builtin_amdgcn_s_memtime();
       if (lane == 0) {
         times[4 * gw + 0] = t_entry;
         times[4 * gw + 1] = t_image;
         times[4 * gw + 2] = t_exit;
-        times[4 * gw + 3] = j0;
+        times[4 * gw + 3] = (uint64_t)j0 | ((c_exit - c_entry) << 24); // tasks | shader cycles
       }
     }
   } else {
@@ -2559,11 +2564,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
       // (ragged batches need their offsets: the probe passes the times array in round_out)
       uint64_t *times = RAGGED ? reinterpret_cast<uint64_t *>(a.round_out) : const_cast<uint64_t *>(a.offsets);
       const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
+      const uint64_t c_exit = __builtin_amdgcn_s_memtime();
       if (lane == 0) {
         times[4 * gw + 0] = t_entry;
         times[4 * gw + 1] = t_image;
         times[4 * gw + 2] = t_exit;
-        times[4 * gw + 3] = j0;
+        times[4 * gw + 3] = (uint64_t)j0 | ((c_exit - c_entry) << 24); // tasks | shader cycles
       }
     }
   }

@@ -98,6 +98,16 @@ for s in $STEPS; do
     bench_c2) run bench_c2 600 python bench.py --config c2 --no-cpu-baseline --no-host-inclusive ;;
     bench_c2_rows) run bench_c2_rows 600 python bench.py --config c2 --ragged-path rows --no-cpu-baseline --no-host-inclusive --no-live-traffic ;;
     timeline) run timeline 300 python tools/probe.py --mode timeline --reps 3 ;;
+    slowcap) # the slow mode: the lease's first processes, clocks read before and after
+           rocm-smi --showclocks --showtemp --showpower > "$OUT/smi_before.txt" 2>&1
+           run tl_c3_first 300 python tools/probe.py --mode timeline --reps 3 --config c3 --steal || exit 1
+           run tl_c3_second 300 python tools/probe.py --mode timeline --reps 3 --config c3 --steal || exit 1
+           run slow_c3_ns 300 python tools/slow_mode.py --config c3 --rounds 2 --blocks 3 --steps 20 --tag c3 || exit 1
+           rocm-smi --showclocks --showtemp --showpower > "$OUT/smi_after.txt" 2>&1 ;;
+    slowclk) # per-wave shader clock beside the launch times (s_memtime / s_memrealtime)
+           run tl_c3_clk 300 python tools/probe.py --mode timeline --reps 8 --config c3 --steal || exit 1
+           run tl_ns_clk 300 python tools/probe.py --mode timeline --reps 8 --config ns --steal || exit 1
+           run tl_c3_clk2 300 python tools/probe.py --mode timeline --reps 8 --config c3 --steal || exit 1 ;;
     timeline_c1) run timeline_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 ;;
     timeline_steal) run timeline_steal_ns 300 python tools/probe.py --mode timeline --reps 3 --steal &&
                     run timeline_steal_c1 300 python tools/probe.py --mode timeline --reps 3 --config c1 --steal ;;

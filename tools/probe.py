@@ -159,9 +159,15 @@ def timeline(w, a):
         e1.record(s)
         w.step()
         torch.cuda.synchronize()
-        t = times.view(nw, 4).cpu().numpy().astype(np.float64)
+        traw = times.view(nw, 4).cpu().numpy()
+        t = traw.astype(np.float64)
         live = t[:, 2] > 0
         t = t[live]
+        # word 3: tasks (low 24 bits) | shader cycles entry -> exit (s_memtime)
+        w3 = traw[live, 3].astype(np.uint64)
+        tasks = (w3 & np.uint64(0xFFFFFF)).astype(np.float64)
+        cyc = (w3 >> np.uint64(24)).astype(np.float64)
+        clk_mhz = cyc / np.maximum(t[:, 2] - t[:, 0], 1.0) * 100.0  # per wave: shader cycles / real 100 MHz ticks
         base = t[:, 0].min()
         ent, img, ext = (t[:, 0] - base) / 100.0, (t[:, 1] - base) / 100.0, (t[:, 2] - base) / 100.0  # us
         pct = lambda x: [round(float(np.percentile(x, q)), 2) for q in (0, 50, 99, 100)]
@@ -178,7 +184,10 @@ def timeline(w, a):
                           "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
                           "entry_us_p0_50_99_100": pct(ent), "image_ready_us": pct(img),
                           "image_copy_us": pct(img - ent), "exit_us": pct(ext),
-                          "tasks_per_wave": pct(t[:, 3])}), flush=True)
+                          "tasks_per_wave": pct(tasks),
+                          "shader_clock_mhz_p0_50_100": [round(float(np.percentile(clk_mhz, q)), 1) for q in (0, 50, 100)],
+                          "shader_clock_mhz_per_xcd": [round(float(np.median(clk_mhz[xcd == x])), 1) for x in range(8)]}),
+              flush=True)
     w.step()
     torch.cuda.synchronize()
     ref = w.out.clone()
