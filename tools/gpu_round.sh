@@ -104,6 +104,15 @@ for s in $STEPS; do
            run tl_c3_second 300 python tools/probe.py --mode timeline --reps 3 --config c3 --steal || exit 1
            run slow_c3_ns 300 python tools/slow_mode.py --config c3 --rounds 2 --blocks 3 --steps 20 --tag c3 || exit 1
            rocm-smi --showclocks --showtemp --showpower > "$OUT/smi_after.txt" 2>&1 ;;
+    slowwrap) # the same 32 GiB read per launch over a 32 GiB vs a 4 GiB buffer (ragged rows kernel), rotated
+           for wv in 32 4 4 32; do
+             run tl_wrap${wv}_$RANDOM 300 python tools/probe.py --mode timeline --reps 6 --config c3 --steal --wrap-gib $wv || exit 1
+           done ;;
+    slowss) # the shader clock in steady state: each timed launch inside 60 ms of back-to-back steps
+           run tl_ns_ss 300 python tools/probe.py --mode timeline --reps 5 --config ns --steal --surround-ms 60 || exit 1
+           run tl_c3_ss 300 python tools/probe.py --mode timeline --reps 5 --config c3 --steal --surround-ms 60 || exit 1
+           run tl_c1_ss 300 python tools/probe.py --mode timeline --reps 5 --config c1 --steal --surround-ms 60 || exit 1
+           run tl_ns_ss2 300 python tools/probe.py --mode timeline --reps 5 --config ns --steal --surround-ms 60 || exit 1 ;;
     slowclk) # per-wave shader clock beside the launch times (s_memtime / s_memrealtime)
            run tl_c3_clk 300 python tools/probe.py --mode timeline --reps 8 --config c3 --steal || exit 1
            run tl_ns_clk 300 python tools/probe.py --mode timeline --reps 8 --config ns --steal || exit 1

@@ -112,6 +112,27 @@ def ablate_variants(w, a):
     return v
 
 
+class WrapWorkload:
+    """C3's launch (8M bodies of 4 KiB, 32 GiB read) as a ragged batch over a
+    buffer of `gib` GiB: body i at (i * 4096) mod gib GiB."""
+
+    def __init__(self, gib):
+        import rpc_amd
+        self.kind, self.L, self.n, self.device = "ragged", 4096, 1 << 23, torch.device("cuda", 0)
+        span = gib << 30
+        self.base = torch.empty(span, dtype=torch.uint8, device=self.device)
+        rpc_amd.fill_random(self.base, 0x5EED0005)
+        i = torch.arange(self.n, dtype=torch.int64, device=self.device)
+        self.offs = (i * 4096) % span
+        self.lens = torch.full((self.n,), 4096, dtype=torch.int32, device=self.device)
+        self.out = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        self.algo_bytes = self.n * (4096 + 16)
+
+    def step(self):
+        import rpc_amd
+        rpc_amd.device_batch(self.base, self.offs, self.lens, out=self.out)
+
+
 def timeline(w, a):
     """Per-wave entry / LDS-image-ready / exit times (s_memrealtime, 100 MHz) of the
     product kernel (kRowsAblTimes variant, exact results) after a clock prewarm:
@@ -151,13 +172,26 @@ def timeline(w, a):
     while time.perf_counter() - t0 < 0.5:
         w.step()
     torch.cuda.synchronize()
+    # --surround-ms: each timed launch sits inside that much back-to-back work on
+    # either side (steady state), not after the host's pause between reps
+    k_around = 1
+    if a.surround_ms > 0:
+        q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        q0.record(s)
+        for _ in range(3):
+            w.step()
+        q1.record(s)
+        q1.synchronize()
+        k_around = max(1, int(a.surround_ms / (q0.elapsed_time(q1) / 3)))
     for rep in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        w.step()
+        for _ in range(k_around):
+            w.step()
         e0.record(s)
         f()
         e1.record(s)
-        w.step()
+        for _ in range(k_around):
+            w.step()
         torch.cuda.synchronize()
         traw = times.view(nw, 4).cpu().numpy()
         t = traw.astype(np.float64)
@@ -178,7 +212,8 @@ def timeline(w, a):
         per_wave_slot = [round(float(np.median(ext[wiw == k])), 1) for k in range(16)]
         if a.save:
             np.save(f"{a.save}_rep{rep}.npy", np.stack([ent, img, ext]))
-        print(json.dumps({"mode": "timeline", "config": a.config, "rep": rep, "qb": qb, "waves": int(live.sum()),
+        print(json.dumps({"mode": "timeline", "config": a.config, "wrap_gib": a.wrap_gib, "surround_steps": k_around,
+                          "rep": rep, "qb": qb, "waves": int(live.sum()),
                           "gshift": a.gshift, "dyn": a.dyn, "steal": a.steal, "exit_median_per_xcd": per_xcd,
                           "exit_median_per_wave_slot": per_wave_slot,
                           "event_us": round(e0.elapsed_time(e1) * 1e3, 1),
@@ -426,6 +461,12 @@ def main():
     ap.add_argument("--steal", action="store_true", help="timeline: DYN with the product's tail stealing")
     ap.add_argument("--steal-pct", type=int, default=3, help="timeline, ragged: pool percent with --steal")
     ap.add_argument("--save", default="", help="timeline: save per-wave times to <save>_rep<k>.npy")
+    ap.add_argument("--surround-ms", type=float, default=0.0,
+                    help="timeline: this many ms of back-to-back product steps before and after each timed launch")
+    ap.add_argument("--wrap-gib", type=int, default=0,
+                    help="timeline: C3's 8M x 4 KiB bodies as a ragged batch whose offsets wrap at this many GiB "
+                         "(32: C3's own footprint; 4: the north star's) -- the same bytes per launch over a smaller "
+                         "address range")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     if a.mode == "packed":
@@ -434,7 +475,7 @@ def main():
         return stream_rows(a)
     if a.mode == "ragged":
         return ragged_ablate(a)
-    w = Workload(a.config, 0, torch.device("cuda", 0))
+    w = Workload(a.config, 0, torch.device("cuda", 0)) if not a.wrap_gib else WrapWorkload(a.wrap_gib)
     if a.mode == "sustain":
         return sustain(w, a)
     if a.mode == "timeline":
