@@ -117,6 +117,8 @@ def test_test_library_exports_the_same_abi():
     assert sorted(line.split()[-1] for line in out.splitlines() if line.strip()) == header_symbols()
     assert b"RPCCRC_TEST_STEAL_GIVEUP" in open(test_lib, "rb").read()
     assert b"RPCCRC_TEST_STEAL_GIVEUP" not in open(LIB, "rb").read()
+    assert b"RPCCRC_TEST_DENSE_ONLY" in open(test_lib, "rb").read()
+    assert b"RPCCRC_TEST_DENSE_ONLY" not in open(LIB, "rb").read()
 
 
 def test_service_stats_without_a_service():

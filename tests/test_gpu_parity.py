@@ -856,6 +856,57 @@ def test_dense_plan_falls_back(case):
         assert np.array_equal(got, want)
 
 
+def test_dense_mode_covers_every_crc():
+    """The dense span step computes EVERY CRC of a dense batch by itself, and the
+    plan refuses a batch that is not dense -- not just "the right
+    answers come back", which the plain rows pass behind the plan would also give.
+    In a child process on the test build with RPCCRC_TEST_DENSE_ONLY=1 that rows
+    pass is left out: the output starts poisoned, every CRC of four dense layouts
+    must then come from the span pass and the fold (oracle), and a batch with a
+    16-B gap must leave the output untouched."""
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import numpy as np, torch, rpc_amd
+from oracle import oracle
+torch.cuda.set_device(0)
+POISON = -0x5A5A5A5B  # 0xA5A5A5A5
+def case(lens, pad=0, gap_at=None, seed=0xD1):
+    lens = np.asarray(lens, dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64) + np.uint64(pad)
+    if gap_at is not None:
+        offs[gap_at:] += np.uint64(16)
+    total = int(offs[-1]) + int(lens[-1])
+    base = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device="cuda:0")
+    rpc_amd.fill_random(base, seed)
+    out = torch.full((lens.size,), POISON, dtype=torch.int32, device="cuda:0")
+    rpc_amd.device_batch(base, torch.from_numpy(offs.view(np.int64)).cuda(), torch.from_numpy(lens.view(np.int32)).cuda(),
+                         out=out, max_len=int(lens.max()))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    return got, oracle.crc32_batch_mt(base.cpu().numpy(), offs, lens)
+rng = np.random.default_rng(0xD0)
+n = 1 << 17
+for name, lens, pad in [("loguniform", oracle.loguniform_lengths(n, 0xD0E6), 0),
+                        ("tiny", rng.integers(64, 101, n), 0),
+                        ("pad9", rng.integers(64, 9000, n), 9),
+                        ("max_body", np.where(np.arange(n) % 997 == 0, 1 << 20, rng.integers(64, 3000, n)), 0)]:
+    got, want = case(lens, pad)
+    print(name, int(np.count_nonzero(got != want)))
+got, want = case(rng.integers(64, 3000, n), gap_at=n // 2)
+print("gap_untouched", bool(np.all(got == np.uint32(0xA5A5A5A5))))
+print("status", rpc_amd.device_status())
+"""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RPCCRC_TEST_DENSE_ONLY="1", PYTHONPATH=repo,
+               RPCCRC_LIB=os.path.join(repo, "rpc_amd", "lib", "librpccrc_test.so"))
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=repo)
+    assert p.returncode == 0, p.stderr[-3000:]
+    for want in ("loguniform 0", "tiny 0", "pad9 0", "max_body 0", "gap_untouched True", "status 0"):
+        assert want in p.stdout, (want, p.stdout)
+
+
 def test_dyn_ragged_batch_with_huge_unrouted_body():
     """a DYN-sized ragged batch whose length bound (64 KiB)
     keeps a 512 MiB body off the big-body route, so ONE wave walks it (~0.1-0.3 s)
