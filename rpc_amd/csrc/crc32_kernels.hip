@@ -1617,10 +1617,12 @@ __global__ __launch_bounds__(1024) void dense_decide_kernel(DenseArgs d, uint32_
 // Nibble map `map` of x from the LDS copy of the maps (crc32_layout.h
 // kDenseTabWords: word (n * 16 + nib) * kDenseMaps + map).
 __device__ __forceinline__ uint32_t dense_map(const uint32_t *t, uint32_t map, uint32_t x) {
-  uint32_t r = 0;
+  uint32_t v[8];
 #pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) r ^= t[(k * 16u + ((x >> (4u * k)) & 15u)) * kDenseMaps + map];
-  return r;
+  for (uint32_t k = 0; k < 8; ++k) v[k] = t[(k * 16u + ((x >> (4u * k)) & 15u)) * kDenseMaps + map];
+  // three-way XORs (v_bitop3_b32): 4 VALU for the 8 lookups instead of 7
+  auto x3 = [](uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); };
+  return x3(x3(v[0], v[1], v[2]), x3(v[3], v[4], v[5]), v[6] ^ v[7]);
 }
 
 // Per boundary g: E = crc0(its block with the bytes from g on zeroed)
@@ -1718,9 +1720,12 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
     const uint32_t hi = off >> 10;
     const uint32_t E = dense_map(s_tab, kDenseMQ + (3u - hi), b.x) ^ b.y;
     const uint32_t En = (uint32_t)__shfl_down((int)E, 1, 64);
+    // (A_{65536 k} with k = 0 is the identity: its 8 lookups are skipped when no
+    // lane of the wave needs k > 0 -- a block distance or body span of >= 16
+    // blocks, i.e. a body over 60 KiB)
     if (lane < K) {
       uint32_t c = dense_map(s_tab, kDenseMB0 + (dist0 & 15u), wi0);
-      c = dense_map(s_tab, kDenseMB1 + (dist0 >> 4), c);
+      if (ballot64(dist0 >= 16u) != 0u) c = dense_map(s_tab, kDenseMB1 + (dist0 >> 4), c);
       __hip_atomic_fetch_xor(&x_acc[own0], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
     for (uint32_t q0 = 64u; q0 < K; q0 += 64u) { // (long bodies)
@@ -1730,7 +1735,7 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
       const uint32_t wi = d.W[min(i, last_w)];
       if (q0 + lane < K) {
         uint32_t c = dense_map(s_tab, kDenseMB0 + (dist & 15u), wi);
-        c = dense_map(s_tab, kDenseMB1 + (dist >> 4), c);
+        if (ballot64(dist >= 16u) != 0u) c = dense_map(s_tab, kDenseMB1 + (dist >> 4), c);
         __hip_atomic_fetch_xor(&x_acc[own], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       }
     }
@@ -1744,7 +1749,8 @@ __global__ __launch_bounds__(1024) void dense_fold_kernel(DenseArgs d) {
       } else {
         const uint32_t D = (uint32_t)(j1 - j); // 1 .. 257
         acc = dense_map(s_tab, kDenseMB0 + (D & 15u), acc ^ wj);
-        acc = dense_map(s_tab, kDenseMB1 + (D >> 4), acc) ^ X ^ Ee;
+        if (ballot64(D >= 16u) != 0u) acc = dense_map(s_tab, kDenseMB1 + (D >> 4), acc);
+        acc ^= X ^ Ee;
       }
       const uint32_t z = 4096u - e_off;
       acc = dense_map(s_tab, kDenseMI0 + (z & 15u), acc);
