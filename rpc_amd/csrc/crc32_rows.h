@@ -421,7 +421,9 @@ constexpr int kRowsRoundOut = 32768;
 // quarter prefix Qp (tests/test_dense_emu.py), from values the lanes hold.
 constexpr int kRowsSpanBnd = 131072;
 // A/B builds of the span pass: RPCCRC_SPAN_TWO_PHASE=1 runs it as two phases
-// (the plain loop, then the pool loop) like host-counted stealing launches;
+// (the plain loop, then the pool loop) like host-counted stealing launches --
+// 2.5 % SLOWER than the one loop (5817 vs 5675 us per C2 span pass, rocprof,
+// rotated A/B, profiles/r06sp), where C3 gained 2.3 % from two phases;
 // RPCCRC_SPAN_ABL=1 never takes the boundary path, 2 also skips the record
 // load (timing only: wrong CRCs).
 #ifndef RPCCRC_SPAN_TWO_PHASE
@@ -2197,6 +2199,12 @@ __global__ void __launch_bounds__(1024, 4) crc32_rows_kernel(ItemsArgs a) {
     };
     if constexpr (STEAL && (!kTwoPhase || (kSpan && !RPCCRC_SPAN_TWO_PHASE))) { // (the span pass is device-counted: one loop)
       rows_phase(std::integral_constant<int, 3>{});
+    } else if constexpr (STEAL && kSpan) {
+      // the dense span pass (device-counted, its pool sized in the kernel): two
+      // phases, and only those two compiled (phase 3 beside them took the
+      // kernel to 128 VGPRs and scratch; these two: 103 VGPRs, no scratch)
+      rows_phase(std::integral_constant<int, 1>{});
+      if (steal) rows_phase(std::integral_constant<int, 2>{});
     } else if constexpr (STEAL) {
       // Device-counted launches (the big-body route's chunk and span passes)
       // keep one loop, as in rounds 2-4: lifted-cap frames ran 1-2 % slower with

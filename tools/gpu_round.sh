@@ -108,6 +108,11 @@ for s in $STEPS; do
            for wv in 32 4 4 32; do
              run tl_wrap${wv}_$RANDOM 300 python tools/probe.py --mode timeline --reps 6 --config c3 --steal --wrap-gib $wv || exit 1
            done ;;
+    survey) # one box: every config's bench line (no PMC / CPU legs) and the steady-state NS clock
+           for c in ns c1 c2 c3 c4; do
+             run survey_$c 300 python bench.py --config $c --no-cpu-baseline --no-host-inclusive --no-live-traffic --no-scalar-latency || exit 1
+           done
+           run survey_tl_ns 300 python tools/probe.py --mode timeline --reps 4 --config ns --steal --surround-ms 60 || exit 1 ;;
     slowss) # the shader clock in steady state: each timed launch inside 60 ms of back-to-back steps
            run tl_ns_ss 300 python tools/probe.py --mode timeline --reps 5 --config ns --steal --surround-ms 60 || exit 1
            run tl_c3_ss 300 python tools/probe.py --mode timeline --reps 5 --config c3 --steal --surround-ms 60 || exit 1
