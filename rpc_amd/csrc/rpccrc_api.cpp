@@ -578,9 +578,10 @@ uint32_t take_test_giveup() {
 }
 
 // Test hook (test build only): RPCCRC_TEST_DENSE_ONLY=1 leaves out the plain
-// rows pass behind a dense plan, so a dense batch's CRCs can only come from the
-// span pass and the fold, and a batch the plan refuses keeps its output as it
-// was (tests/test_gpu_parity.py test_dense_mode_covers_every_crc).
+// rows pass of ragged batches, so a dense batch's CRCs can only come from the
+// span pass and the fold, and a batch that does not take the dense step (the
+// plan refuses it, or it is too small for it) keeps its output as it was
+// (tests/test_gpu_parity.py test_dense_mode_covers_every_crc).
 bool test_dense_only() {
 #ifdef RPCCRC_TEST_HOOKS
   static const bool v = [] {
@@ -858,7 +859,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   StealLease rsl; // the plain rows pass deals its tail from a steal counter too (RPCCRC_RAGGED_STEAL=0: not)
   if (split) {
     RPCCRC_TRY(launch_split_batch(a, ws.ptr(), split_bytes, nt, mb, s));
-  } else if (!route_all && !(dense && test_dense_only())) {
+  } else if (!route_all && !test_dense_only()) {
     if (ragged_steal()) {
       if (const int rc = rsl.get(c, n, 1, s)) return rc;
       a.steal = rsl.p;

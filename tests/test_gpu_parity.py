@@ -798,15 +798,16 @@ def test_dense_span_mode(case):
     oracle and against the rows path: log-uniform 64 B - 64 KiB (C2's shape), runs
     of 64-100 B bodies (> 6 boundaries a block: the record's overflow path), bodies
     ending exactly on block boundaries (and the stream's end on one), a stream
-    starting 7 B into its buffer (the anchor rounds down to 16 B), 1 MiB bodies (the
-    fold's longest Horner) and alternating runs of tiny and large bodies."""
+    starting 7 B into its buffer (the anchor rounds down to 16 B), 240 KiB bodies (the
+    longest a bounded batch sends through the step: a bound of 256 KiB or more takes the
+    big-body route) and alternating runs of tiny and large bodies."""
     rng = np.random.default_rng(hash(case) & 0xFFFF)
     n = 1 << 17
     if case == "loguniform":
         lens = oracle.loguniform_lengths(n, 0xD0E5)
         _dense_case(lens)
-    elif case == "tiny_dense":
-        _dense_case(rng.integers(64, 101, n).astype(np.uint32))
+    elif case == "tiny_dense":  # (4M bodies: the step needs >= 8 DYN rounds of blocks per workgroup)
+        _dense_case(rng.integers(64, 101, 1 << 22).astype(np.uint32))
     elif case == "block_ends":
         lens = np.full(n, 4096, dtype=np.uint32)
         lens[0::3] = 4032
@@ -815,9 +816,9 @@ def test_dense_span_mode(case):
         _dense_case(lens)
     elif case == "pad7":
         _dense_case(rng.integers(64, 5000, n).astype(np.uint32), pad=7)
-    elif case == "max_body":
+    elif case == "max_body":  # (60-block bodies; a bound >= 256 KiB takes the big-body route instead)
         lens = rng.integers(64, 3000, n).astype(np.uint32)
-        lens[::997] = 1 << 20
+        lens[::997] = 240 << 10
         _dense_case(lens)
     else:
         lens = np.where((np.arange(n) // 500) % 2 == 0, rng.integers(64, 128, n),
@@ -862,8 +863,10 @@ def test_dense_mode_covers_every_crc():
     answers come back", which the plain rows pass behind the plan would also give.
     In a child process on the test build with RPCCRC_TEST_DENSE_ONLY=1 that rows
     pass is left out: the output starts poisoned, every CRC of four dense layouts
-    must then come from the span pass and the fold (oracle), and a batch with a
-    16-B gap must leave the output untouched."""
+    must then come from the span pass and the fold (oracle; 64-100 B bodies: 4M
+    of them, for the >= 8 DYN rounds of blocks per workgroup the step needs),
+    and a batch with a 16-B gap, or too small for the step, must leave the
+    output untouched."""
     import os
     import subprocess
     import sys
@@ -889,13 +892,20 @@ def case(lens, pad=0, gap_at=None, seed=0xD1):
 rng = np.random.default_rng(0xD0)
 n = 1 << 17
 for name, lens, pad in [("loguniform", oracle.loguniform_lengths(n, 0xD0E6), 0),
-                        ("tiny", rng.integers(64, 101, n), 0),
+                        ("tiny", rng.integers(64, 101, 1 << 22), 0),
                         ("pad9", rng.integers(64, 9000, n), 9),
-                        ("max_body", np.where(np.arange(n) % 997 == 0, 1 << 20, rng.integers(64, 3000, n)), 0)]:
+                        # bodies of 60 blocks (the fold's A_{65536 k} maps; a bound >= 256 KiB would
+                        # send the batch through the big-body route instead)
+                        ("max_body", np.where(np.arange(n) % 997 == 0, 240 << 10, rng.integers(64, 3000, n)), 0),
+                        # the bound allows the step, the stream is small (2.1K blocks, counted on the device)
+                        ("small_stream", np.where(np.arange(n) == 5, 240 << 10, 64), 3)]:
     got, want = case(lens, pad)
     print(name, int(np.count_nonzero(got != want)))
 got, want = case(rng.integers(64, 3000, n), gap_at=n // 2)
 print("gap_untouched", bool(np.all(got == np.uint32(0xA5A5A5A5))))
+# too small for the dense step (< 8 DYN rounds of 4 KiB blocks per workgroup): not taken
+got, want = case(rng.integers(64, 101, n))
+print("small_untouched", bool(np.all(got == np.uint32(0xA5A5A5A5))))
 print("status", rpc_amd.device_status())
 """
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -903,7 +913,9 @@ print("status", rpc_amd.device_status())
                RPCCRC_LIB=os.path.join(repo, "rpc_amd", "lib", "librpccrc_test.so"))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=repo)
     assert p.returncode == 0, p.stderr[-3000:]
-    for want in ("loguniform 0", "tiny 0", "pad9 0", "max_body 0", "gap_untouched True", "status 0"):
+    for want in ("loguniform 0", "tiny 0", "pad9 0", "max_body 0", "small_stream 0", "gap_untouched True",
+                 "small_untouched True",
+                 "status 0"):
         assert want in p.stdout, (want, p.stdout)
 
 
