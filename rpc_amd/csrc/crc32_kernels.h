@@ -166,6 +166,10 @@ struct BigRoute {
   // takes the route, body b = batch index b (no classify pass, no b_idx list,
   // no plain rows pass); the plan sums the lengths itself.
   uint32_t all_n = 0;
+  // Dense span mode beside the route: non-zero *skip (the dense
+  // plan's DenseCtl::skip) makes the classify pass route no body, so the route's
+  // later passes find nothing to do.  nullptr: no dense plan.
+  const uint32_t *skip = nullptr;
   const uint32_t *tq = nullptr;  // Tq[q] = A_q(0xFFFFFFFF): the combine seeds chunk 0 with it
   // Span mode (route-all only; span_rows_max > 0, the batch base 4 KiB-aligned):
   // when the plan finds the bodies dense in [base, base + 4096 * span_rows_max)

@@ -681,8 +681,9 @@ __global__ void __launch_bounds__(256) big_classify_kernel(const uint32_t *lengt
                                                              BigRoute r) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
+  const bool dense = r.skip != nullptr && *r.skip != 0u; // (uniform) the dense step has every body
   const uint32_t len = (i < n) ? lengths[i] : 0u;
-  const bool big = i < n && len >= big_min;
+  const bool big = !dense && i < n && len >= big_min;
   const uint64_t m = __builtin_amdgcn_ballot_w64(big);
   uint64_t routed = 0;
   if (m != 0) { // wave-uniform: one slot claim per wave

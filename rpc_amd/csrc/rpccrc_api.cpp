@@ -789,6 +789,33 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   Lease ws;
   if (split_bytes + route_bytes > 0)
     if (const int rc = ws.get(c.ws, split_bytes + route_bytes, s)) return rc;
+  // Dense span mode: a ragged batch of many bodies whose bound
+  // (or, unbounded, the mode's own 1 MiB body limit) allows it.  The plan
+  // decides on the device whether the bodies lie back to back in order with
+  // 64 B .. 1 MiB each; then the span pass and the fold compute every CRC, and
+  // the rows pass and the big-body route's classify pass (so the whole route)
+  // have nothing to do (DenseCtl::skip); otherwise the span pass and the fold
+  // exit at once.
+  const uint64_t dense_len = max_len ? max_len : kDenseMaxBody;
+  const uint64_t nb_cap = std::min<uint64_t>(n * dense_len / 4096u + 2u, kDenseMaxBlocks);
+  const bool dense = dense_enabled() && !route_all && !split && !small_bodies && mode == kModeFinal &&
+                     n >= kDenseMinN && n <= kDenseMaxN && dense_len >= kDenseMinBody && dense_len <= kDenseMaxBody &&
+                     nb_cap >= 8ull * dyn_round(1) * (uint64_t)mb;
+  Lease dws;
+  DenseArgs dn{};
+  StealLease dsl; // the span pass's steal counter
+  if (dense) {
+    if (const int rc = dws.get(c.ws, dense_workspace_bytes(n, nb_cap), s)) return rc;
+    dn = dense_carve(dws.ptr(), n, nb_cap);
+    dn.base = base;
+    dn.offsets = offsets;
+    dn.lengths = lengths;
+    dn.out = out;
+    dn.tq = c.tq;
+    dn.tab = c.dense_tab;
+    RPCCRC_TRY(launch_dense_plan(dn, s));
+    a.skip_dev = &dn.ctl->skip;
+  }
   BigRoute r{};
   StealLease sl;  // the route's chunk pass deals its tail from this counter (device-counted)
   StealLease ssl; // ... and its span pass from this one
@@ -820,6 +847,7 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
       }
     } else {
       const uint32_t big_min = big_min_for(n);
+      if (dense) r.skip = &dn.ctl->skip;
       RPCCRC_TRY(launch_big_classify(lengths, n, big_min, r, s));
       a.routed = r.routed;
       a.big_min = big_min;
@@ -831,30 +859,6 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
     if (span_rows)
       if (const int rc = ssl.get(c, span_rows, 1, s)) return rc;
     a.test_giveup = take_test_giveup(); // (the route's chunk pass; the plain rows pass takes its own below)
-  }
-  // Dense span mode: a bounded batch (no big-body route) of
-  // many bodies whose bound allows it.  The plan decides on the device whether
-  // the bodies lie back to back in order with 64 B .. 1 MiB each; then the span
-  // pass and the fold compute every CRC and the rows pass below exits at once
-  // (DenseCtl::skip); otherwise the span pass and the fold exit at once.
-  const uint64_t nb_cap = std::min<uint64_t>(n * (uint64_t)max_len / 4096u + 2u, kDenseMaxBlocks);
-  const bool dense = dense_enabled() && !route && !split && !small_bodies && mode == kModeFinal && n >= kDenseMinN &&
-                     n <= kDenseMaxN && max_len >= kDenseMinBody && max_len <= kDenseMaxBody &&
-                     nb_cap >= 8ull * dyn_round(1) * (uint64_t)mb;
-  Lease dws;
-  DenseArgs dn{};
-  StealLease dsl; // the span pass's steal counter
-  if (dense) {
-    if (const int rc = dws.get(c.ws, dense_workspace_bytes(n, nb_cap), s)) return rc;
-    dn = dense_carve(dws.ptr(), n, nb_cap);
-    dn.base = base;
-    dn.offsets = offsets;
-    dn.lengths = lengths;
-    dn.out = out;
-    dn.tq = c.tq;
-    dn.tab = c.dense_tab;
-    RPCCRC_TRY(launch_dense_plan(dn, s));
-    a.skip_dev = &dn.ctl->skip;
   }
   StealLease rsl; // the plain rows pass deals its tail from a steal counter too (RPCCRC_RAGGED_STEAL=0: not)
   if (split) {

@@ -875,7 +875,7 @@ import numpy as np, torch, rpc_amd
 from oracle import oracle
 torch.cuda.set_device(0)
 POISON = -0x5A5A5A5B  # 0xA5A5A5A5
-def case(lens, pad=0, gap_at=None, seed=0xD1):
+def case(lens, pad=0, gap_at=None, seed=0xD1, bound=None):
     lens = np.asarray(lens, dtype=np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64) + np.uint64(pad)
     if gap_at is not None:
@@ -885,7 +885,7 @@ def case(lens, pad=0, gap_at=None, seed=0xD1):
     rpc_amd.fill_random(base, seed)
     out = torch.full((lens.size,), POISON, dtype=torch.int32, device="cuda:0")
     rpc_amd.device_batch(base, torch.from_numpy(offs.view(np.int64)).cuda(), torch.from_numpy(lens.view(np.int32)).cuda(),
-                         out=out, max_len=int(lens.max()))
+                         out=out, max_len=int(lens.max()) if bound is None else bound)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32)
     return got, oracle.crc32_batch_mt(base.cpu().numpy(), offs, lens)
@@ -901,6 +901,12 @@ for name, lens, pad in [("loguniform", oracle.loguniform_lengths(n, 0xD0E6), 0),
                         ("small_stream", np.where(np.arange(n) == 5, 240 << 10, 64), 3)]:
     got, want = case(lens, pad)
     print(name, int(np.count_nonzero(got != want)))
+# the plain (unbounded) call, and a bound over the big-body route's threshold
+# with 300 KiB bodies: the route's classify pass leaves every body to the step
+got, want = case(oracle.loguniform_lengths(n, 0xD0E7), bound=0)
+print("unbounded", int(np.count_nonzero(got != want)))
+got, want = case(np.where(np.arange(n) % 499 == 0, 300 << 10, rng.integers(64, 3000, n)), bound=1 << 20)
+print("over_route_bound", int(np.count_nonzero(got != want)))
 got, want = case(rng.integers(64, 3000, n), gap_at=n // 2)
 print("gap_untouched", bool(np.all(got == np.uint32(0xA5A5A5A5))))
 # too small for the dense step (< 8 DYN rounds of 4 KiB blocks per workgroup): not taken
@@ -913,7 +919,8 @@ print("status", rpc_amd.device_status())
                RPCCRC_LIB=os.path.join(repo, "rpc_amd", "lib", "librpccrc_test.so"))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=repo)
     assert p.returncode == 0, p.stderr[-3000:]
-    for want in ("loguniform 0", "tiny 0", "pad9 0", "max_body 0", "small_stream 0", "gap_untouched True",
+    for want in ("loguniform 0", "tiny 0", "pad9 0", "max_body 0", "small_stream 0", "unbounded 0",
+                 "over_route_bound 0", "gap_untouched True",
                  "small_untouched True",
                  "status 0"):
         assert want in p.stdout, (want, p.stdout)
