@@ -108,6 +108,13 @@ for s in $STEPS; do
            for wv in 32 4 4 32; do
              run tl_wrap${wv}_$RANDOM 300 python tools/probe.py --mode timeline --reps 6 --config c3 --steal --wrap-gib $wv || exit 1
            done ;;
+    firstproc) # the lease's first processes: the same north-star line three times, then C3 twice
+           for k in 1 2 3; do
+             run fp_ns_$k 300 python bench.py --no-cpu-baseline --no-host-inclusive --no-live-traffic --no-scalar-latency || exit 1
+           done
+           for k in 1 2; do
+             run fp_c3_$k 300 python bench.py --config c3 --no-cpu-baseline --no-host-inclusive --no-live-traffic --no-scalar-latency || exit 1
+           done ;;
     survey) # one box: every config's bench line (no PMC / CPU legs) and the steady-state NS clock
            for c in ns c1 c2 c3 c4; do
              run survey_$c 300 python bench.py --config $c --no-cpu-baseline --no-host-inclusive --no-live-traffic --no-scalar-latency || exit 1
