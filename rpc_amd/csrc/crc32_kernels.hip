@@ -1516,6 +1516,11 @@ __global__ __launch_bounds__(256) void dense_plan_kernel(DenseArgs d) {
   const uint64_t nblocks = (rel_n + 4095u) >> 12;
   constexpr uint64_t kNone = ~(uint64_t)0; // past boundary n: a block of its own
   bool bad = nblocks > d.nb_cap || nblocks > kDenseMaxBlocks;
+  // records are written below rec_lim only: the array holds nb_cap of them, and
+  // a batch the plan refuses (a longer stream than the bound allowed, or bodies
+  // before the first one: offsets that wrap below the anchor) must not write
+  // past it -- its records are never read
+  const uint64_t rec_lim = min(nblocks, (uint64_t)d.nb_cap);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x / 64u) + (threadIdx.x >> 6);
   const uint64_t g0 = 64u * w, g = g0 + lane;
@@ -1554,13 +1559,13 @@ __global__ __launch_bounds__(256) void dense_plan_kernel(DenseArgs d) {
       const uint32_t qb = (uint32_t)__shfl((int)(uint32_t)(rb & 4095u), (int)(src & 63u), 64);
       o[i] = i < cnt ? (src < 64u ? qa : qb) : 0u;
     }
-    if (va && first && ja < nblocks)
+    if (va && first && ja < rec_lim)
       d.rec[ja] = make_uint4((uint32_t)g | (min(cnt, 64u) << 25), o[0] | (o[1] << 16), o[2] | (o[3] << 16),
                              o[4] | (o[5] << 16));
     // empty blocks (jp, ja) before a first boundary: k records, dealt over the wave
     uint32_t k = 0;
     if (va && first && g != 0 && ja > jp + 1u && ja - jp <= (kDenseMaxBody >> 12) + 2)
-      k = (uint32_t)(min(ja, nblocks) > jp + 1u ? min(ja, nblocks) - jp - 1u : 0u);
+      k = (uint32_t)(min(ja, rec_lim) > jp + 1u ? min(ja, rec_lim) - jp - 1u : 0u);
     const uint32_t incl = wave_incl_scan<false>(k);
     const uint32_t K = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     // the first pass's owners by marks and a max-scan (fold kernel), later
@@ -1587,7 +1592,7 @@ __global__ __launch_bounds__(256) void dense_plan_kernel(DenseArgs d) {
       const uint64_t jp_o = shfl64(jp, (int)own);
       const uint32_t ex_o = (uint32_t)__shfl((int)(incl - k), (int)own, 64);
       const uint64_t j = jp_o + 1u + (q - ex_o);
-      if (q < K && j < nblocks) d.rec[j] = make_uint4((uint32_t)(g0 + own), 0u, 0u, 0u);
+      if (q < K && j < rec_lim) d.rec[j] = make_uint4((uint32_t)(g0 + own), 0u, 0u, 0u);
     }
   }
   const int any_bad = __syncthreads_or(bad ? 1 : 0);

@@ -796,8 +796,11 @@ int ragged(const DeviceCtx &c, const uint8_t *base, const uint64_t *offsets, con
   // the rows pass and the big-body route's classify pass (so the whole route)
   // have nothing to do (DenseCtl::skip); otherwise the span pass and the fold
   // exit at once.
+  // nb_cap: the blocks the workspace holds (20 B each) -- by the bound, or for an
+  // unbounded call by a 64 KiB average body (a longer stream is refused by the
+  // plan and takes the rows pass and the route: exact, as without the mode)
   const uint64_t dense_len = max_len ? max_len : kDenseMaxBody;
-  const uint64_t nb_cap = std::min<uint64_t>(n * dense_len / 4096u + 2u, kDenseMaxBlocks);
+  const uint64_t nb_cap = std::min<uint64_t>(n * (max_len ? max_len : 65536u) / 4096u + 2u, kDenseMaxBlocks);
   const bool dense = dense_enabled() && !route_all && !split && !small_bodies && mode == kModeFinal &&
                      n >= kDenseMinN && n <= kDenseMaxN && dense_len >= kDenseMinBody && dense_len <= kDenseMaxBody &&
                      nb_cap >= 8ull * dyn_round(1) * (uint64_t)mb;

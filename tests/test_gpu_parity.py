@@ -826,11 +826,13 @@ def test_dense_span_mode(case):
         _dense_case(lens)
 
 
-@pytest.mark.parametrize("case", ["gap", "short_body", "long_body", "unordered"])
+@pytest.mark.parametrize("case", ["gap", "short_body", "long_body", "unordered", "reversed"])
 def test_dense_plan_falls_back(case):
     """A bounded ragged batch the dense plan must refuse -- a 16-B gap between two
-    bodies, a 63-B body, a body over 1 MiB, bodies out of order -- is CRC'd by the
-    rows pass instead (decided on the device): every CRC against the oracle."""
+    bodies, a 63-B body, a body over 1 MiB, bodies out of order, the whole batch in
+    reverse (every offset below the first body's: stream offsets that wrap, which
+    the plan must not use to write records) -- is CRC'd by the rows pass instead
+    (decided on the device): every CRC against the oracle."""
     rng = np.random.default_rng(7)
     n = 1 << 17
     lens = rng.integers(64, 3000, n).astype(np.uint32)
@@ -845,7 +847,10 @@ def test_dense_plan_falls_back(case):
     else:
         offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
         perm = np.arange(n)
-        perm[[10, 11]] = perm[[11, 10]]
+        if case == "unordered":
+            perm[[10, 11]] = perm[[11, 10]]
+        else:
+            perm = perm[::-1].copy()
         offs, lens2 = offs[perm].copy(), lens[perm].copy()
         total = int(lens.sum(dtype=np.uint64))
         base = torch.empty((total + 7) // 8 * 8, dtype=torch.uint8, device=DEV)
@@ -907,6 +912,18 @@ got, want = case(oracle.loguniform_lengths(n, 0xD0E7), bound=0)
 print("unbounded", int(np.count_nonzero(got != want)))
 got, want = case(np.where(np.arange(n) % 499 == 0, 300 << 10, rng.integers(64, 3000, n)), bound=1 << 20)
 print("over_route_bound", int(np.count_nonzero(got != want)))
+# unbounded, a stream longer than the workspace's 64 KiB-per-body estimate (2^16
+# bodies of 100 KiB: 1.6M blocks against 1M): refused, so left to the rows pass
+nb = 1 << 16
+lens_b = np.full(nb, 100 << 10, dtype=np.uint32)
+offs_b = np.arange(nb, dtype=np.uint64) * np.uint64(100 << 10)
+base_b = torch.zeros(nb * (100 << 10), dtype=torch.uint8, device="cuda:0")
+out_b = torch.full((nb,), POISON, dtype=torch.int32, device="cuda:0")
+rpc_amd.device_batch(base_b, torch.from_numpy(offs_b.view(np.int64)).cuda(), torch.from_numpy(lens_b.view(np.int32)).cuda(),
+                     out=out_b)
+torch.cuda.synchronize()
+print("over_cap_untouched", bool(torch.all(out_b == POISON).item()))
+del base_b
 got, want = case(rng.integers(64, 3000, n), gap_at=n // 2)
 print("gap_untouched", bool(np.all(got == np.uint32(0xA5A5A5A5))))
 # too small for the dense step (< 8 DYN rounds of 4 KiB blocks per workgroup): not taken
@@ -920,7 +937,7 @@ print("status", rpc_amd.device_status())
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=repo)
     assert p.returncode == 0, p.stderr[-3000:]
     for want in ("loguniform 0", "tiny 0", "pad9 0", "max_body 0", "small_stream 0", "unbounded 0",
-                 "over_route_bound 0", "gap_untouched True",
+                 "over_route_bound 0", "over_cap_untouched True", "gap_untouched True",
                  "small_untouched True",
                  "status 0"):
         assert want in p.stdout, (want, p.stdout)
