@@ -78,7 +78,10 @@ RPCCRC_API int64_t rpc_crc32_verify_batch(const uint8_t *base, const uint64_t *o
  * are device pointers on the current device.  Asynchronous on `stream`.
  * Bodies of >= 256 KiB (>= 16 KiB in batches of <= 16384 bodies) are cut into
  * chunks on the device and folded with the GF(2) combine, so one long body does
- * not serialise the batch on one wave. */
+ * not serialise the batch on one wave.  A batch of >= 65536 bodies that lie back
+ * to back in batch order (each 64 B - 1 MiB; decided on the device) is CRC'd as
+ * one stream of 4 KiB blocks and folded per body (dense span mode, DESIGN.md 4.9;
+ * RPCCRC_DENSE=0 turns it off).  Same results either way. */
 RPCCRC_API int rpc_crc32_device_batch(const uint8_t *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
                            uint64_t n, uint32_t *d_out, void *stream);
 

@@ -677,7 +677,7 @@ bool ragged_steal() {
   return v;
 }
 
-// Dense span mode for bounded ragged batches.  RPCCRC_DENSE=0
+// Dense span mode for ragged device batches.  RPCCRC_DENSE=0
 // turns it off (the rows pass only, as in rounds 1-5).
 bool dense_enabled() {
   static const bool v = [] {
