@@ -90,6 +90,7 @@ def parse():
                         "median then comes from a second K-step pass with an event after every step. 1: per-step "
                         "events in the timed pass itself (each event is a marker packet between launches: "
                         "+4 us per C1 step, profiles/r02/r02aj_step_events_ab.txt)")
+    p.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)  # live_traffic's PMC child
     p.add_argument("--prewarm-s", type=float, default=0.5,
                    help="untimed steps before the W warmup steps until this much time has passed: the GPU "
                         "clock ramps over the first ~20 launches of sustained load (DESIGN.md 5)")
@@ -629,9 +630,13 @@ def live_traffic(args, algo_bytes: int):
             cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "3",
                    "--warmup", "1", "--prewarm-s", "0", "--no-cpu-baseline", "--no-host-inclusive",
-                   "--no-live-traffic"] + (["--ragged-path", args.ragged_path] if args.ragged_path != "auto" else [])
+                   "--no-live-traffic", "--traffic-child"] + (["--ragged-path", args.ragged_path] if args.ragged_path != "auto" else [])
             try:
-                p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+                # (a one-process group of the parent's launcher would make the child
+                # rendezvous on its port: the child runs outside any group)
+                env = {k: v for k, v in os.environ.items()
+                       if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+                p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
             except subprocess.TimeoutExpired:
                 return None, f"rocprofv3 --pmc {counter} timed out"
             if p.returncode != 0:
@@ -864,6 +869,12 @@ def main():
         median_src = "second K-step pass with an event after every step (each adds a marker between launches)"
     tr = rank_timing(dist, device, wall, kernel_s, median_s, w.total)
     tmax, total_bytes = tr["wall"], tr["total"]
+    if args.traffic_child:
+        # live_traffic's PMC child: only the product's steps in the trace (no
+        # stream probe, unbounded call or CRC check launches to tell apart)
+        if dist:
+            dist.destroy_process_group()
+        return
     # every rank checks its own first bodies (outside the timed region)
     log("per-rank CRC check against the reference crc.c")
     chk = reduce_crc_check(dist, device, rank_crc_check(*rank_check_sample(w),
